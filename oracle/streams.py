@@ -1,0 +1,47 @@
+"""Legacy-MT19937 random streams in the reference's per-step consumption order.
+
+The reference draws every random number from NumPy's global legacy RandomState
+(SURVEY.md App. A-7).  Per chain-step, in order:
+  gauss proposal (callable Delta of norm.rvs, e.g. examples/mcmc/mcmc_prob2.py:31):
+      d x standard_normal (scipy norm.rvs = loc + scale*z), in Delta keyword order
+  sphere proposal (tuple delta, field.py:516):   uniform(size=d)  -> d raw doubles
+  uniform proposal (list delta, variable.py:633): d x uniform     -> d raw doubles
+  then 1 x random_sample for the MH threshold t (sp_utils.py:30-31, sp.py:249)
+  gibbs (cond_cov.py:57-59 via vtypes.py:185-186): 1 x random_sample, no threshold.
+Standard normals are stored as z; uniforms as the raw random_sample double u in
+[0, 1) (numpy's legacy uniform(lo, hi) is lo + (hi - lo) * u).
+
+Layout: [T][R][N] float64 (step, draw, chain) -- the replay layout the engine
+reads (chain index fastest, so a wavefront's loads coalesce).
+"""
+import numpy as np
+
+
+def stream_width(spec):
+  """Draws per chain-step R."""
+  if spec['proposal']['kind'] == 'gibbs':
+    return 1
+  return int(spec['dim']) + 1
+
+
+def legacy_streams(spec, seeds, n_steps):
+  """Per-chain np.random.RandomState(seed) streams, shape [T, R, N]."""
+  seeds = np.asarray(seeds).reshape(-1)
+  n, d, r = seeds.size, int(spec['dim']), stream_width(spec)
+  kind = spec['proposal']['kind']
+  out = np.empty((n_steps, r, n), dtype=np.float64)
+  for c, seed in enumerate(seeds):
+    rs = np.random.RandomState(int(seed))
+    col = out[:, :, c]
+    if kind == 'gibbs':
+      col[:, 0] = rs.random_sample(n_steps)
+      continue
+    for t in range(n_steps):
+      if kind == 'gauss':
+        # d separate norm.rvs calls == one standard_normal(d): the polar
+        # method's cached second deviate persists across calls either way.
+        col[t, :d] = rs.standard_normal(d)
+      else:
+        col[t, :d] = rs.random_sample(d)
+      col[t, d] = rs.random_sample()
+  return out

@@ -1,0 +1,181 @@
+"""Specs of the golden workloads (tools/gen_golden.py) as plain dicts.
+
+Each builder restates, in the spec vocabulary of probayes_amd/spec.py, the
+reference model that tools/gen_golden.py ran (cited per entry).  The dicts are
+complete (every key the engine reads), so tests hand them unchanged to the
+oracle and to the engine.  TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+"""
+import json
+import os
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))), 'tests', 'golden')
+
+NEARLY_NEGATIVE_INF = -1.7976931348623158e+308
+
+
+def load_golden(name):
+  with np.load(os.path.join(GOLDEN_DIR, name + '.npz'),
+               allow_pickle=False) as z:
+    g = {k: z[k] for k in z.files}
+  g['meta'] = json.loads(str(g['meta']))
+  return g
+
+
+def _spec(dim, names, target, proposal, scores='hastings', pscale='log',
+          tran=None, prior=None, ufun=None):
+  d = dim
+  return {'dim': d, 'names': list(names), 'pscale': pscale, 'target': target,
+          'proposal': proposal, 'scores': scores,
+          'tran': tran or {'kind': 'const', 'value': 1.0, 'sym': True},
+          'prior': prior,
+          'ufun': np.zeros(d, np.int32) if ufun is None else
+                  np.asarray(ufun, np.int32)}
+
+
+def _gauss(d, scale, loc=0., order=None):
+  return {'kind': 'gauss', 'loc': np.broadcast_to(np.float64(loc), (d,)).copy()
+          if np.ndim(loc) == 0 else np.asarray(loc, np.float64),
+          'scale': np.full(d, float(scale)),
+          'order': np.arange(d, dtype=np.int32) if order is None else
+                   np.asarray(order, np.int32)}
+
+
+def _qpdf(d, scale, order, offset=None, sym=True):
+  return {'kind': 'gauss_pdf', 'scale': float(scale), 'sym': sym,
+          'order': np.asarray(order, np.int32),
+          'offset': np.zeros(d) if offset is None else
+                    np.asarray(offset, np.float64)}
+
+
+def spec_metrohast_norm1d(params):
+  """examples/mcmc/metrohast_norm1d.py:22-35: mu in [40,60], sigma in [5,20]
+  with (log, exp) ufun; tuple delta (0.005,) scale=True; tran (1., 1.) tuple;
+  joint=True uniform root prior, iid obs."""
+  mu_len = 60. - 40.
+  ul = np.log(np.array([5., 20.]))                  # variable.py:332-335
+  sg_len = max(ul) - min(ul)
+  lengths = np.array([mu_len, sg_len])
+  rss = np.sqrt(np.sum(lengths ** 2))               # field.py:513-515
+  prior_logp = -np.log(mu_len) + -np.log(sg_len)    # rv.py:160, rf_utils.py:10-42
+  return _spec(2, ['mu', 'sigma'],
+               {'kind': 'norm_iid', 'obs': params['x_obs'], 'loc': 0,
+                'scale': 1},
+               {'kind': 'sphere', 'delta': 0.005 * rss, 'lengths': lengths},
+               tran={'kind': 'const', 'value': 1.0, 'sym': False},
+               prior={'lo': np.array([40., 5.]), 'hi': np.array([60., 20.]),
+                      'lo_incl': np.array([1, 1], np.int32),
+                      'hi_incl': np.array([1, 1], np.int32),
+                      'logp': float(prior_logp)},
+               ufun=[0, 1])
+
+
+def spec_mcmc_prob2(params):
+  """examples/mcmc/mcmc_prob2.py:24-31."""
+  return _spec(1, ['x'], {'kind': 'norm_pdf', 'loc': np.array([2.]),
+                          'scale': np.array([np.sqrt(2)])},
+               _gauss(1, 1.), pscale='lin', tran=_qpdf(1, 1., [0]))
+
+
+def spec_mcmc_prob3(params):
+  """examples/mcmc/mcmc_prob3.py:32-39."""
+  return _spec(1, ['x'], {'kind': 'uniform_pdf', 'lo': np.array([3.]),
+                          'scale': np.array([4.])},
+               _gauss(1, 1.), pscale='lin', tran=_qpdf(1, 1., [0]))
+
+
+_COV4 = np.array([[2.0, 1.2], [1.2, 2.0]])
+
+
+def spec_mcmc_prob4a(params):
+  """examples/mcmc/mcmc_prob4a.py:37-48 (q multiplies the y pdf first)."""
+  return _spec(2, ['x', 'y'], {'kind': 'mvn', 'mean': np.zeros(2),
+                               'cov': _COV4},
+               _gauss(2, 1.), pscale='lin', tran=_qpdf(2, 1., [1, 0]))
+
+
+def spec_mcmc_prob4b(params):
+  """examples/mcmc/mcmc_prob4b.py:34-51."""
+  return _spec(2, ['x', 'y'], {'kind': 'uniform_pdf', 'lo': np.array([3., 1.]),
+                               'scale': np.array([4., 8.])},
+               _gauss(2, 1.), pscale='lin', tran=_qpdf(2, 1., [1, 0]))
+
+
+def spec_mcmc_prob6(params):
+  """examples/mcmc/mcmc_prob6.py:48-61: tran (q, r) tuple -> asymmetric, but
+  reval_tran returns q (rf.py:536), delta loc (-2, 0)."""
+  return _spec(2, ['x', 'y'], {'kind': 'mvn', 'mean': np.zeros(2),
+                               'cov': _COV4},
+               _gauss(2, 1., loc=[-2., 0.]), pscale='lin',
+               tran=_qpdf(2, 1., [1, 0], offset=[2., 0.], sym=False))
+
+
+def _gibbs(mean, cov, lo, hi, names):
+  d = len(mean)
+  return _spec(d, names, {'kind': 'mvn', 'mean': np.asarray(mean, np.float64),
+                          'cov': np.asarray(cov, np.float64)},
+               {'kind': 'gibbs', 'mean': np.asarray(mean, np.float64),
+                'cov': np.asarray(cov, np.float64),
+                'lo': np.full(d, float(lo)), 'hi': np.full(d, float(hi)),
+                'tsteps': 1},
+               scores='gibbs', pscale='lin')
+
+
+def spec_gibbs_norm2d(params):
+  """examples/mcmc/gibbs_norm2d.py:9-19."""
+  return _gibbs([0.5, -0.5], [[1.5, -1.0], [-1.0, 2.]], -10., 10., ['x', 'y'])
+
+
+def spec_gibbs8(params):
+  """SURVEY App. B H4 (cfg3 shape)."""
+  return _gibbs(params['mean'], params['cov'], -20., 20.,
+                ['x{}'.format(i) for i in range(8)])
+
+
+def spec_diag10(params):
+  """SURVEY App. B H3 (cfg2 shape)."""
+  d = len(params['mu'])
+  return _spec(d, ['x{}'.format(i) for i in range(d)],
+               {'kind': 'diag_gauss', 'mu': np.asarray(params['mu'], float),
+                'sigma': np.asarray(params['sigma'], float)},
+               _gauss(d, float(params['step'])))
+
+
+def spec_gmm2(params):
+  """SURVEY App. B H5 (cfg5 shape)."""
+  return _spec(2, ['x', 'y'],
+               {'kind': 'gmm', 'logw': np.log(np.asarray(params['w'], float)),
+                'mu': np.asarray(params['mu'], float),
+                'sd': np.asarray(params['sd'], float)},
+               _gauss(2, float(params['step'])))
+
+
+INITS = {
+    'metrohast_norm1d': [50., 12.5], 'mcmc_prob2': [0.], 'mcmc_prob3': [5.],
+    'mcmc_prob4a': [0., 1.], 'mcmc_prob4b': [5., 5.], 'mcmc_prob6': [0., 1.],
+    'gibbs_norm2d': [0., 1.], 'diag10': [0.] * 10, 'gibbs8': [0.] * 8,
+    'gmm2': [0., 0.],
+}
+
+WORKLOADS = {
+    'metrohast_norm1d': spec_metrohast_norm1d, 'mcmc_prob2': spec_mcmc_prob2,
+    'mcmc_prob3': spec_mcmc_prob3, 'mcmc_prob4a': spec_mcmc_prob4a,
+    'mcmc_prob4b': spec_mcmc_prob4b, 'mcmc_prob6': spec_mcmc_prob6,
+    'gibbs_norm2d': spec_gibbs_norm2d, 'diag10': spec_diag10,
+    'gibbs8': spec_gibbs8, 'gmm2': spec_gmm2,
+}
+
+
+def golden_params(g):
+  return {k[len('param_'):]: v for k, v in g.items() if k.startswith('param_')}
+
+
+def golden_spec(name, g=None):
+  g = load_golden(name) if g is None else g
+  return WORKLOADS[name](golden_params(g))
+
+
+def golden_init(name, n):
+  return np.tile(np.asarray(INITS[name], np.float64), (n, 1))

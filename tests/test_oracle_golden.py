@@ -1,0 +1,44 @@
+"""Pins the CPU oracle to the reference: every golden workload recorded by
+tools/gen_golden.py (which ran probayes 0.0.8 itself) must be reproduced
+BIT-FOR-BIT by oracle.run_mh / oracle.run_gibbs on the same legacy streams."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle.workloads import golden_init
+
+
+@pytest.mark.parametrize('name', sorted(oracle.WORKLOADS))
+def test_oracle_matches_reference_bitwise(name):
+  g = oracle.load_golden(name)
+  spec = oracle.golden_spec(name, g)
+  n, t = g['v_x'].shape[:2]
+  streams = oracle.legacy_streams(spec, g['seeds'], t)
+  run = oracle.run_gibbs if spec['scores'] == 'gibbs' else oracle.run_mh
+  out = run(spec, golden_init(name, n), streams)
+  keys = ['v_x', 'v_p', 'p_x', 'p_p', 'u']
+  if spec['scores'] != 'gibbs':
+    keys += ['s', 't']
+  for k in keys:
+    np.testing.assert_array_equal(out[k], g[k], err_msg='{}:{}'.format(name, k))
+
+
+def test_golden_fixture_metadata():
+  for name in oracle.WORKLOADS:
+    g = oracle.load_golden(name)
+    assert g['meta']['name'] == name
+    assert g['meta']['generator'] == 'tools/gen_golden.py'
+    assert len(g['seeds']) == g['v_x'].shape[0]
+
+
+def test_streams_layout_and_determinism():
+  spec = oracle.golden_spec('diag10')
+  a = oracle.legacy_streams(spec, [5, 6], 4)
+  b = oracle.legacy_streams(spec, [5, 6], 4)
+  assert a.shape == (4, 11, 2)
+  np.testing.assert_array_equal(a, b)
+  rs = np.random.RandomState(6)
+  z = rs.standard_normal(10)
+  u = rs.random_sample()
+  np.testing.assert_array_equal(a[0, :10, 1], z)
+  assert a[0, 10, 1] == u
