@@ -1,0 +1,191 @@
+/*
+ * pbhip.h -- C-ABI of libpbhip.so, the MI355X (gfx950) batched
+ * Metropolis-Hastings / CondCov-Gibbs engine behind probayes_amd.
+ *
+ * The reference (probayes 0.0.8) has no C/FFI layer: its boundary is the pure
+ * Python SP API.  Each entry point below replaces one piece of the per-chain
+ * Python call stack of SP.next (sp.py:221-258) for N chains at once; the
+ * reference interface it stands in for is cited beside it.  Bindings: the
+ * ctypes stub in probayes_amd/_lib.py (and INTEGRATION.md).
+ *
+ * Conventions
+ *  - Every function returns int status: 0 = PBH_OK, < 0 = error; the message
+ *    is in pbh_last_error() (thread-local).  No function throws or aborts.
+ *  - Host buffers are caller-allocated; the engine owns every device buffer.
+ *  - One engine per device, calls on one engine must not be concurrent.
+ *    Multi-GPU = one process (or thread) per device + pbh_rccl_*.
+ *  - Chain-major arrays on the host are [chain][dim]; device and trace arrays
+ *    are dim-major with the chain index fastest ([step][dim][chain]).
+ *  - All arithmetic is IEEE fp64 (constants.py:7 DEFAULT_FP_PRECISION = 64).
+ */
+#ifndef PBHIP_H
+#define PBHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBH_ABI_VERSION 1
+#define PBH_MAX_DIM 32
+
+#define PBH_OK 0
+#define PBH_ERR_ARG (-1)
+#define PBH_ERR_HIP (-2)
+#define PBH_ERR_STATE (-3)
+#define PBH_ERR_UNSUPPORTED (-4)
+#define PBH_ERR_RCCL (-5)
+
+/* Joint density forms the engine lowers. */
+enum pbh_target_kind {
+  PBH_TARGET_DIAG_GAUSS = 1,  /* sum_i norm.logpdf(x_i, mu_i, sigma_i)        */
+  PBH_TARGET_NORM_IID = 2,    /* np.sum(norm.logpdf(obs, x[loc], x[scale]))   */
+  PBH_TARGET_GMM = 3,         /* logsumexp_k(logw_k + sum_i logpdf(x_i,mu_ki,sd_k)) */
+  PBH_TARGET_NORM_PDF = 4,    /* prod_i norm.pdf(x_i, loc_i, scale_i)          */
+  PBH_TARGET_UNIFORM_PDF = 5, /* prod_i uniform.pdf(x_i, lo_i, scale_i)        */
+  PBH_TARGET_MVN = 6          /* multivariate_normal.pdf at the permuted x     */
+};
+enum pbh_pscale { PBH_PSCALE_LOG = 0, PBH_PSCALE_LIN = 1 };
+enum pbh_scores {
+  PBH_SCORES_HASTINGS = 1, PBH_SCORES_METROPOLIS = 2, PBH_SCORES_GIBBS = 3
+};
+enum pbh_tran_kind { PBH_TRAN_CONST = 1, PBH_TRAN_GAUSS_PDF = 2 };
+enum pbh_proposal_kind {
+  PBH_PROP_GAUSS = 1,   /* callable Delta(norm.rvs(loc, scale)) per dim        */
+  PBH_PROP_SPHERE = 2,  /* tuple delta, field.py:509-531                      */
+  PBH_PROP_UNIFORM = 3, /* list delta, variable.py:625-633                    */
+  PBH_PROP_GIBBS = 4    /* CondCov conditional draw, cond_cov.py:42-65        */
+};
+enum pbh_rng_mode {
+  PBH_RNG_REPLAY = 0, /* randoms read from a caller-supplied [T][R][N] stream  */
+  PBH_RNG_PHILOX = 1  /* Philox-4x32-10 keyed by (seed, global chain id)      */
+};
+
+/* Joint density + acceptance (replaces RF.set_prob/set_tran + SP.set_scores:
+ * rf.py:91,169; sp.py:57-100; prob.py:331-380; rf_utils.py:10-42).
+ * All pointers are host pointers, copied into device memory by the call.   */
+typedef struct pbh_model {
+  int32_t dim;          /* d, 1..PBH_MAX_DIM                                  */
+  int32_t target_kind;  /* enum pbh_target_kind                               */
+  int32_t pscale;       /* enum pbh_pscale of the density (pscales.py:21-41)   */
+  int32_t scores;       /* enum pbh_scores (sp_utils.py:87-91)                */
+  /* target parameters (meaning per kind):
+   *   DIAG_GAUSS : a = mu[d], b = sigma[d], c = log(sigma)[d]
+   *   NORM_IID   : a = obs[n], n = n_obs, i0 = loc dim, i1 = scale dim
+   *   GMM        : a = logw[K], b = mu[K*d], c = sd[K], e = log(sd)[K], n = K
+   *   NORM_PDF   : a = loc[d], b = scale[d]
+   *   UNIFORM_PDF: a = lo[d], b = scale[d]
+   *   MVN        : a = mean[d] (in permuted order), b = prec_U[d*d] row-major,
+   *                c = {rank*log(2pi) + log_pdet}, perm = permutation[d]      */
+  const double *a, *b, *c, *e;
+  const int32_t *perm;
+  int64_t n;
+  int32_t i0, i1;
+  /* joint=True uniform root prior (rv_utils.py:8-47); has_prior = 0/1 */
+  int32_t has_prior;
+  const double *prior_lo, *prior_hi;
+  const int32_t *prior_lo_incl, *prior_hi_incl;
+  double prior_logp;
+  /* per-dim change of variable: 1 = (log, exp) ufun (variable.py:693-697) */
+  const int32_t *ufun;
+  /* transition q(x'|x) (rf.py:169-239, 490-538) */
+  int32_t tran_kind;    /* enum pbh_tran_kind                                 */
+  int32_t tran_sym;     /* 1 = symmetric (r = None), 0 = tuple tran           */
+  double tran_value;    /* CONST: value of q                                  */
+  double tran_scale;    /* GAUSS_PDF: sigma                                   */
+  const double *tran_offset;  /* GAUSS_PDF: loc offset per dim               */
+  const int32_t *tran_order;  /* GAUSS_PDF: multiplication order of dims     */
+} pbh_model;
+
+/* Proposal (replaces RF.set_delta / Field.eval_delta / apply_delta:
+ * field.py:220-317, 469-552; variable.py:600-739).                         */
+typedef struct pbh_proposal {
+  int32_t kind;             /* enum pbh_proposal_kind (not GIBBS)            */
+  const double *loc;        /* GAUSS: loc[d]                                  */
+  const double *scale;      /* GAUSS: scale[d]                                */
+  const int32_t *order;     /* GAUSS: dim receiving the j-th draw             */
+  double delta;             /* SPHERE: delta (already * rss if scale=True)    */
+  const double *lengths;    /* SPHERE: per-dim multiplier (lengths or 1)      */
+  const double *delta_vec;  /* UNIFORM: delta[d]                              */
+} pbh_proposal;
+
+/* CondCov Gibbs tables (replaces CondCov.__init__ + RF.eval_tfun cycling:
+ * cond_cov.py:22-39, rf.py:446-458).  Precomputed on the host like the
+ * reference does (np.linalg.inv, norm.cdf).                                  */
+typedef struct pbh_gibbs {
+  const double *mean;   /* mu[d]                                             */
+  const double *coef;   /* coef[d*(d-1)]: row i = Sigma_{i,-i} Sigma_{-i,-i}^-1 */
+  const double *stdv;   /* conditional sd[d]                                 */
+  const double *cdf;    /* cdf limits [d*2] (lo, hi)                         */
+  int32_t tsteps;       /* coordinates per SP step (rf.py:446-452)            */
+} pbh_gibbs;
+
+typedef struct pbh_engine pbh_engine;
+
+/* ---- engine lifetime ---------------------------------------------------- */
+const char *pbh_last_error(void);
+int pbh_abi_version(void);
+int pbh_device_count(int *count);
+int pbh_create(int device, pbh_engine **out);
+int pbh_destroy(pbh_engine *eng);
+
+/* ---- model ------------------------------------------------------------- */
+int pbh_set_model(pbh_engine *eng, const pbh_model *model);
+int pbh_set_proposal(pbh_engine *eng, const pbh_proposal *prop);
+int pbh_set_gibbs(pbh_engine *eng, const pbh_gibbs *gibbs);
+
+/* ---- chains and randomness (SP.sampler(init, ...): sp.py:261-278) ------- */
+/* Allocates chain state for chains [chain_offset, chain_offset + n) and copies
+ * init [n][d]; the first pbh_run step proposes from init and auto-accepts
+ * (sp_utils.py:24-25, App. A-3).                                            */
+int pbh_init_chains(pbh_engine *eng, int64_t n_chains, int64_t chain_offset,
+                    const double *init);
+int pbh_set_rng(pbh_engine *eng, int32_t mode, uint64_t seed);
+/* Replay stream [n_steps][R][n_chains] (R = d + 1 for MH, 1 for Gibbs),
+ * consumed from the next pbh_run step on.                                   */
+int pbh_upload_replay(pbh_engine *eng, int64_t n_steps, const double *rand);
+int pbh_stream_width(pbh_engine *eng, int32_t *r);
+
+/* ---- running (SP.walk / sample_generator: sp.py:281-295, sp_utils.py:8-16) */
+/* Device trace ring for the next runs: every thin-th step is recorded.
+ * debug = 1 also records proposals p_x, p_p and the score s.               */
+int pbh_alloc_trace(pbh_engine *eng, int64_t capacity, int32_t thin,
+                    int32_t debug);
+/* Launches n_steps chain-steps on the engine stream (asynchronous);
+ * steps_per_launch bounds one kernel's fused step loop (0 = all).          */
+int pbh_run(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
+int pbh_sync(pbh_engine *eng);
+/* Kernel-only time of the last pbh_run (HIP events on the engine stream). */
+int pbh_last_run_ms(pbh_engine *eng, double *ms, int64_t *launches);
+
+/* ---- results (SP.__call__(samples) summary: sp.py:131-198) -------------- */
+int pbh_get_state(pbh_engine *eng, double *x, double *logp);
+int pbh_trace_len(pbh_engine *eng, int64_t *n_recorded);
+/* Copies recorded steps [first, first + n) of the trace:
+ * x [n][d][N], logp [n][N], acc [n][ceil(N/64)] accept bitmask words
+ * (bit j of word w = chain 64 w + j).  Optional debug buffers may be NULL. */
+int pbh_get_trace(pbh_engine *eng, int64_t first, int64_t n, double *x,
+                  double *logp, uint64_t *acc, double *p_x, double *p_p,
+                  double *s);
+/* Per-chain running moments over every step since the last reset:
+ * sum[d][N], sumsq[d][N] of the accepted state, n_acc[N] accepts.          */
+int pbh_get_moments(pbh_engine *eng, double *sum, double *sumsq,
+                    int64_t *n_acc, int64_t *n_steps);
+int pbh_reset_moments(pbh_engine *eng);
+
+/* ---- multi-GPU: one RCCL all-gather over xGMI --------- */
+int pbh_rccl_unique_id(uint8_t id[128]);
+int pbh_rccl_init(pbh_engine *eng, int32_t rank, int32_t world,
+                  const uint8_t id[128]);
+/* Gathers every rank's moments ([2d+1][N_local] doubles, n_acc as double)
+ * into out [world][2d+1][N_local] on the host.                              */
+int pbh_rccl_allgather_moments(pbh_engine *eng, double *out);
+/* Max-reduces one double over ranks (bench timing).                         */
+int pbh_rccl_allreduce_max(pbh_engine *eng, double *value);
+int pbh_rccl_destroy(pbh_engine *eng);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBHIP_H */

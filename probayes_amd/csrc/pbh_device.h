@@ -1,0 +1,248 @@
+// pbh_device.h -- device arithmetic for the gfx950 MH / Gibbs kernels.
+//
+// Everything here is IEEE fp64 and is compiled with -ffp-contract=off so that
+// each expression rounds exactly like the NumPy/SciPy expression it restates
+// (replay-mode parity with the reference, SURVEY.md §7 "hard parts").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbh {
+
+// constants.py:9-35 (64-bit precision)
+constexpr double kNearlyPosZero = 2.2250738585072014e-308;
+constexpr double kNearlyPosInf = 1.7976931348623158e+308;
+constexpr double kNearlyNegInf = -1.7976931348623158e+308;
+// np.log(NEARLY_POSITIVE_INF), passed in from the host (bit-identical to the
+// reference's LOG_NEARLY_POSITIVE_INF) via KArgs::log_npi.
+
+// scipy.stats._continuous_distns: _norm_pdf_C = sqrt(2 pi), _norm_pdf_logC
+// = log(_norm_pdf_C); both evaluated by NumPy on the host, passed as doubles.
+
+// ---------------------------------------------------------------------------
+// Philox-4x32-10 (Salmon et al., SC'11), the production RNG.  Counter-based:
+// the stream of chain c at step g is a pure function of (seed, c, g), so
+// traces are identical for any sharding of chains over GPUs.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
+                                                uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// 53-bit double in [0, 1) from two words, the same construction as NumPy's
+// legacy random_sample: ((a >> 5) * 2^26 + (b >> 6)) / 2^53.
+__device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) *
+         (1.0 / 9007199254740992.0);
+}
+
+// Two standard normals from one Philox block (Box-Muller, sincospi form).
+__device__ __forceinline__ void box_muller(u32x4 w, double &z0, double &z1) {
+  const double u1 = 1.0 - u01(w.x, w.y);  // (0, 1]
+  const double u2 = u01(w.z, w.w);
+  const double r = sqrt(-2.0 * log(u1));
+  double s, c;
+  sincospi(2.0 * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// ---------------------------------------------------------------------------
+// NumPy pairwise summation (numpy/_core/src/umath/loops_utils.h.src
+// pairwise_sum, numpy 2.2): < 8 terms sequential from 0, <= 128 terms with
+// eight interleaved accumulators, larger blocks split at n2 = n/2 - (n/2)%8.
+// np.sum == this for contiguous float64 (checked in tests on the host).
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ double np_sum_regs(const double (&a)[N], int n) {
+  // n <= N <= 128, compile-time unrolled with wave-uniform predicates.
+  if (n < 8) {
+    double res = 0.;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (i < n) res += a[i];
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (j < N) ? a[j < N ? j : 0] : 0.;
+  const int full = n - (n % 8);
+#pragma unroll
+  for (int i = 8; i < N; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i + j < N && i < full) r[j] += a[(i + j) < N ? (i + j) : 0];
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (i >= full && i < n) res += a[i];
+  return res;
+}
+
+// Pairwise sum of f(j) for j in [0, n) with f evaluated on the fly (the iid
+// observation reduction PD.prod, pd.py:368).  Leaves of <= 128 terms use the
+// 8-accumulator block; the split tree is walked with an explicit stack.
+template <class F>
+__device__ __forceinline__ double np_leaf(F f, int64_t s, int64_t n) {
+  if (n < 8) {
+    double res = 0.;
+    for (int64_t i = 0; i < n; ++i) res += f(s + i);
+    return res;
+  }
+  double r0 = f(s), r1 = f(s + 1), r2 = f(s + 2), r3 = f(s + 3);
+  double r4 = f(s + 4), r5 = f(s + 5), r6 = f(s + 6), r7 = f(s + 7);
+  int64_t i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += f(s + i);
+    r1 += f(s + i + 1);
+    r2 += f(s + i + 2);
+    r3 += f(s + i + 3);
+    r4 += f(s + i + 4);
+    r5 += f(s + i + 5);
+    r6 += f(s + i + 6);
+    r7 += f(s + i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += f(s + i);
+  return res;
+}
+
+template <class F>
+__device__ double np_pairwise(F f, int64_t n) {
+  if (n <= 128) return np_leaf(f, 0, n);
+  // Post-order walk of numpy's recursion.  Depth <= 48 for any int64 n.
+  int64_t st_s[48], st_n[48];
+  double st_v[48];
+  int st_state[48];
+  int sp = 0;
+  st_s[0] = 0; st_n[0] = n; st_state[0] = 0;
+  double ret = 0.;
+  while (sp >= 0) {
+    const int64_t s = st_s[sp], m = st_n[sp];
+    if (m <= 128) {
+      ret = np_leaf(f, s, m);
+      --sp;
+      continue;
+    }
+    int64_t m2 = m / 2;
+    m2 -= m2 % 8;
+    if (st_state[sp] == 0) {           // descend left
+      st_state[sp] = 1;
+      ++sp;
+      st_s[sp] = s; st_n[sp] = m2; st_state[sp] = 0;
+    } else if (st_state[sp] == 1) {    // left done -> descend right
+      st_v[sp] = ret;
+      st_state[sp] = 2;
+      ++sp;
+      st_s[sp] = s + m2; st_n[sp] = m - m2; st_state[sp] = 0;
+    } else {                           // both done
+      ret = st_v[sp] + ret;
+      --sp;
+    }
+  }
+  return ret;
+}
+
+// ---------------------------------------------------------------------------
+// scipy.special.ndtri: Cephes ndtri.c (S. L. Moshier), the algorithm scipy
+// 1.15 ships; the coefficients below reproduce scipy's ndtri bit-for-bit on
+// the host (tests/test_device_math.py) -- on the device up to log/sqrt ulps.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double ndtri(double y0) {
+  constexpr double s2pi = 2.50662827463100050242E0;
+  constexpr double P0[5] = {-5.99633501014107895267E1, 9.80010754185999661536E1,
+                            -5.66762857469070293439E1, 1.39312609387279679503E1,
+                            -1.23916583867381258016E0};
+  constexpr double Q0[8] = {1.95448858338141759834E0, 4.67627912898881538453E0,
+                            8.63602421390890590575E1, -2.25462687854119370527E2,
+                            2.00260212380060660359E2, -8.20372256168333339912E1,
+                            1.59056225126211695515E1, -1.18331621121330003142E0};
+  constexpr double P1[9] = {4.05544892305962419923E0, 3.15251094599893866154E1,
+                            5.71628192246421288162E1, 4.40805073893200834700E1,
+                            1.46849561928858024014E1, 2.18663306850790267539E0,
+                            -1.40256079171354495875E-1, -3.50424626827848203418E-2,
+                            -8.57456785154685413611E-4};
+  constexpr double Q1[8] = {1.57799883256466749731E1, 4.53907635128879210584E1,
+                            4.13172038254672030440E1, 1.50425385692907503408E1,
+                            2.50464946208309415979E0, -1.42182922854787788574E-1,
+                            -3.80806407691578277194E-2, -9.33259480895457427372E-4};
+  constexpr double P2[9] = {3.23774891776946035970E0, 6.91522889068984211695E0,
+                            3.93881025292474443415E0, 1.33303460815807542389E0,
+                            2.01485389549179081538E-1, 1.23716634817820021358E-2,
+                            3.01581553508235416007E-4, 2.65806974686737550832E-6,
+                            6.23974539184983293730E-9};
+  constexpr double Q2[8] = {6.02427039364742014255E0, 3.67983563856160859403E0,
+                            1.37702099489081330271E0, 2.16236993594496635890E-1,
+                            1.34204006088543189037E-2, 3.28014464682127739104E-4,
+                            2.89247864745380683936E-6, 6.79019408009981274425E-9};
+  if (y0 == 0.0) return -__builtin_inf();
+  if (y0 == 1.0) return __builtin_inf();
+  if (y0 < 0.0 || y0 > 1.0) return __builtin_nan("");
+  bool negate = true;
+  double y = y0;
+  if (y > (1.0 - 0.13533528323661269189)) {
+    y = 1.0 - y;
+    negate = false;
+  }
+  if (y > 0.13533528323661269189) {
+    y = y - 0.5;
+    const double y2 = y * y;
+    double p = P0[0];
+#pragma unroll
+    for (int i = 1; i < 5; ++i) p = p * y2 + P0[i];
+    double q = y2 + Q0[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) q = q * y2 + Q0[i];
+    double x = y + y * (y2 * p / q);
+    return x * s2pi;
+  }
+  const double x = sqrt(-2.0 * log(y));
+  const double x0 = x - log(x) / x;
+  const double z = 1.0 / x;
+  double p, q;
+  if (x < 8.0) {
+    p = P1[0];
+#pragma unroll
+    for (int i = 1; i < 9; ++i) p = p * z + P1[i];
+    q = z + Q1[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) q = q * z + Q1[i];
+  } else {
+    p = P2[0];
+#pragma unroll
+    for (int i = 1; i < 9; ++i) p = p * z + P2[i];
+    q = z + Q2[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) q = q * z + Q2[i];
+  }
+  const double x1 = z * p / q;
+  const double r = x0 - x1;
+  return negate ? -r : r;
+}
+
+// pscales.py:56-65 exp_logp (scalar branch).
+__device__ __forceinline__ double exp_logp(double lp, double log_npi) {
+  return (lp <= log_npi) ? exp(lp) : kNearlyPosInf;
+}
+
+// np.maximum(NEARLY_POSITIVE_ZERO, b): NaN propagates.
+__device__ __forceinline__ double np_max_tiny(double b) {
+  return (b != b) ? b : (b >= kNearlyPosZero ? b : kNearlyPosZero);
+}
+
+}  // namespace pbh

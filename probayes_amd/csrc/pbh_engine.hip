@@ -1,0 +1,740 @@
+// pbh_engine.hip -- the C-ABI of include/pbhip.h: engine state, device
+// memory, launches, HIP-event timing and the RCCL trace all-gather.
+//
+// The engine owns every device buffer; the caller passes host pointers.
+// Nothing here throws across the C boundary: errors become status codes with
+// a thread-local message (pbh_last_error).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pbhip.h"
+#include "pbh_kernels.h"
+
+using pbh::KArgs;
+
+struct pbh_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // model / proposal / gibbs (device constant blocks)
+  bool has_model = false, has_prop = false, has_gibbs = false;
+  int d = 0;
+  KArgs k{};
+  double *dmodel = nullptr, *dprop = nullptr, *dgibbs = nullptr;
+  std::vector<int32_t> draw_order;  // GAUSS: dim receiving the j-th draw
+  // chains
+  int64_t n = 0, off = 0;
+  double *x = nullptr, *lp = nullptr;
+  bool has_pred = false;
+  int64_t g = 0;  // chain-steps done since pbh_init_chains
+  // randomness
+  int32_t rng = PBH_RNG_PHILOX;
+  uint64_t seed = 0;
+  double *rep = nullptr;
+  int64_t rep_steps = 0, rep_g0 = 0;
+  // trace
+  int64_t cap = 0;
+  int32_t thin = 1, debug = 0;
+  int64_t rec_base = 0;
+  double *tx = nullptr, *tlp = nullptr, *tpx = nullptr, *tpp = nullptr,
+         *ts = nullptr;
+  uint64_t *tacc = nullptr;
+  // moments
+  double *msum = nullptr, *msq = nullptr;
+  int64_t *nacc = nullptr;
+  int64_t mom_steps = 0;
+  // timing of the last pbh_run
+  bool timed = false;
+  int64_t last_launches = 0;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int32_t rank = 0, world = 1;
+  double *gather_send = nullptr, *gather_recv = nullptr, *scalar = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return fail(PBH_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                       \
+  do {                                                                       \
+    ncclResult_t _r = (expr);                                                \
+    if (_r != ncclSuccess)                                                   \
+      return fail(PBH_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+template <class T>
+void dfree(T *&p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+template <class T>
+int dalloc(T *&p, size_t count) {
+  dfree(p);
+  if (count == 0) return PBH_OK;
+  HIP_TRY(hipMalloc((void **)&p, count * sizeof(T)));
+  return PBH_OK;
+}
+
+int upload(double *&dst, const std::vector<double> &h, hipStream_t s) {
+  int rc = dalloc(dst, h.size() ? h.size() : 1);
+  if (rc) return rc;
+  if (h.size())
+    HIP_TRY(hipMemcpyAsync(dst, h.data(), h.size() * sizeof(double),
+                           hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return PBH_OK;
+}
+
+// Appends host array a[0:n] to a packed block; returns its offset.
+size_t pack(std::vector<double> &blk, const double *a, int64_t n) {
+  const size_t o = blk.size();
+  for (int64_t i = 0; i < n; ++i) blk.push_back(a[i]);
+  return o;
+}
+
+int check_ptr(const void *p, const char *name) {
+  return p ? PBH_OK : fail(PBH_ERR_ARG, "%s must not be NULL", name);
+}
+
+__global__ void pack_moments(const double *sum, const double *sq,
+                             const int64_t *nacc, double *out, int64_t dn,
+                             int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < dn) {
+    out[i] = sum[i];
+    out[dn + i] = sq[i];
+  }
+  if (i < n) out[2 * dn + i] = (double)nacc[i];
+}
+
+void free_trace(pbh_engine *e) {
+  dfree(e->tx); dfree(e->tlp); dfree(e->tpx); dfree(e->tpp); dfree(e->ts);
+  dfree(e->tacc);
+  e->cap = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *pbh_last_error(void) { return g_err.c_str(); }
+
+int pbh_abi_version(void) { return PBH_ABI_VERSION; }
+
+int pbh_device_count(int *count) {
+  if (check_ptr(count, "count")) return PBH_ERR_ARG;
+  HIP_TRY(hipGetDeviceCount(count));
+  return PBH_OK;
+}
+
+int pbh_create(int device, pbh_engine **out) {
+  if (check_ptr(out, "out")) return PBH_ERR_ARG;
+  *out = nullptr;
+  int nd = 0;
+  HIP_TRY(hipGetDeviceCount(&nd));
+  if (device < 0 || device >= nd)
+    return fail(PBH_ERR_ARG, "device %d out of range (%d devices)", device, nd);
+  HIP_TRY(hipSetDevice(device));
+  pbh_engine *e = new pbh_engine();
+  e->device = device;
+  hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (err == hipSuccess) err = hipEventCreate(&e->ev0);
+  if (err == hipSuccess) err = hipEventCreate(&e->ev1);
+  if (err != hipSuccess) {
+    delete e;
+    return fail(PBH_ERR_HIP, "stream/event creation failed: %s",
+                hipGetErrorString(err));
+  }
+  *out = e;
+  return PBH_OK;
+}
+
+int pbh_destroy(pbh_engine *e) {
+  if (!e) return PBH_OK;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->comm) ncclCommDestroy(e->comm);
+  dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
+  dfree(e->x); dfree(e->lp); dfree(e->rep);
+  free_trace(e);
+  dfree(e->msum); dfree(e->msq); dfree(e->nacc);
+  dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// model
+// ---------------------------------------------------------------------------
+int pbh_set_model(pbh_engine *e, const pbh_model *m) {
+  if (check_ptr(e, "engine") || check_ptr(m, "model")) return PBH_ERR_ARG;
+  const int d = m->dim;
+  if (d < 1 || d > PBH_MAX_DIM)
+    return fail(PBH_ERR_ARG, "dim %d outside 1..%d", d, PBH_MAX_DIM);
+  if (!pbh::mh_dim_supported(d))
+    return fail(PBH_ERR_UNSUPPORTED,
+                "dim %d has no compiled kernel (1-12, 16, 20, 24, 32)", d);
+  if (m->pscale != PBH_PSCALE_LOG && m->pscale != PBH_PSCALE_LIN)
+    return fail(PBH_ERR_ARG, "bad pscale %d", m->pscale);
+  if (m->scores < PBH_SCORES_HASTINGS || m->scores > PBH_SCORES_GIBBS)
+    return fail(PBH_ERR_ARG, "bad scores %d", m->scores);
+  if (e->x && d != e->d)
+    return fail(PBH_ERR_STATE, "dim %d differs from initialised chains (%d)",
+                d, e->d);
+  std::vector<double> blk;
+  size_t oa = 0, ob = 0, oc = 0, oe = 0, oplo = 0, ophi = 0, otoff = 0;
+  const double *A = m->a, *B = m->b, *C = m->c, *E = m->e;
+  int64_t na = 0, nb = 0, nc = 0, ne = 0;
+  switch (m->target_kind) {
+    case PBH_TARGET_DIAG_GAUSS: na = nb = nc = d; break;
+    case PBH_TARGET_NORM_IID:
+      if (m->n < 1) return fail(PBH_ERR_ARG, "NORM_IID needs n_obs >= 1");
+      if (m->i0 < 0 || m->i0 >= d || m->i1 < 0 || m->i1 >= d)
+        return fail(PBH_ERR_ARG, "NORM_IID loc/scale dims out of range");
+      na = m->n;
+      break;
+    case PBH_TARGET_GMM:
+      if (m->n < 1) return fail(PBH_ERR_ARG, "GMM needs K >= 1");
+      na = m->n; nb = m->n * d; nc = ne = m->n;
+      break;
+    case PBH_TARGET_NORM_PDF:
+    case PBH_TARGET_UNIFORM_PDF: na = nb = d; break;
+    case PBH_TARGET_MVN: na = d; nb = (int64_t)d * d; nc = 1; break;
+    default: return fail(PBH_ERR_ARG, "bad target kind %d", m->target_kind);
+  }
+  if ((na && !A) || (nb && !B) || (nc && !C) || (ne && !E))
+    return fail(PBH_ERR_ARG, "target arrays missing for kind %d",
+                m->target_kind);
+  oa = pack(blk, A, na); ob = pack(blk, B, nb); oc = pack(blk, C, nc);
+  oe = pack(blk, E, ne);
+  uint32_t lo_incl = 0, hi_incl = 0, ufun = 0;
+  if (m->has_prior) {
+    if (!m->prior_lo || !m->prior_hi || !m->prior_lo_incl || !m->prior_hi_incl)
+      return fail(PBH_ERR_ARG, "prior arrays missing");
+    oplo = pack(blk, m->prior_lo, d);
+    ophi = pack(blk, m->prior_hi, d);
+    for (int i = 0; i < d; ++i) {
+      if (m->prior_lo_incl[i]) lo_incl |= 1u << i;
+      if (m->prior_hi_incl[i]) hi_incl |= 1u << i;
+    }
+  }
+  if (m->ufun)
+    for (int i = 0; i < d; ++i)
+      if (m->ufun[i]) ufun |= 1u << i;
+  int tran_rev = 0;
+  if (m->tran_kind == PBH_TRAN_GAUSS_PDF) {
+    if (!m->tran_offset) return fail(PBH_ERR_ARG, "tran_offset missing");
+    otoff = pack(blk, m->tran_offset, d);
+    if (m->tran_order) {
+      bool ident = true, rev = true;
+      for (int i = 0; i < d; ++i) {
+        ident = ident && m->tran_order[i] == i;
+        rev = rev && m->tran_order[i] == d - 1 - i;
+      }
+      if (!ident && !rev)
+        return fail(PBH_ERR_UNSUPPORTED,
+                    "tran_order must be the identity or reversed");
+      tran_rev = ident ? 0 : 1;
+    }
+  } else if (m->tran_kind != PBH_TRAN_CONST) {
+    return fail(PBH_ERR_ARG, "bad tran kind %d", m->tran_kind);
+  }
+  if (blk.empty()) blk.push_back(0.);
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = upload(e->dmodel, blk, e->stream);
+  if (rc) return rc;
+  KArgs &k = e->k;
+  const double *base = e->dmodel;
+  k.d = d; k.target = m->target_kind; k.pscale = m->pscale; k.scores = m->scores;
+  k.ta = base + oa; k.tb = base + ob; k.tc = base + oc; k.te = base + oe;
+  k.tn = (m->target_kind == PBH_TARGET_NORM_IID || m->target_kind == PBH_TARGET_GMM) ? m->n : 0;
+  k.i0 = m->i0; k.i1 = m->i1;
+  k.has_prior = m->has_prior ? 1 : 0;
+  k.plo = base + oplo; k.phi = base + ophi;
+  k.plo_incl = lo_incl; k.phi_incl = hi_incl;
+  k.prior_logp = m->prior_logp;
+  k.ufun = ufun;
+  k.tran_kind = m->tran_kind; k.tran_sym = m->tran_sym ? 1 : 0; k.tran_rev = tran_rev;
+  k.tran_value = m->tran_value; k.tran_scale = m->tran_scale;
+  k.tran_off = base + otoff;
+  // Constants the reference evaluates with NumPy on the host; the IEEE
+  // results of these host libm calls are what the kernels compare against.
+  k.log_npi = std::log(1.7976931348623158e+308);
+  k.norm_C = std::sqrt(2 * M_PI);
+  k.norm_logC = std::log(k.norm_C);
+  e->d = d;
+  e->has_model = true;
+  return PBH_OK;
+}
+
+int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
+  if (check_ptr(e, "engine") || check_ptr(p, "proposal")) return PBH_ERR_ARG;
+  if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
+  const int d = e->d;
+  std::vector<double> blk;
+  size_t oloc = 0, oscl = 0, olen = 0, odel = 0;
+  e->draw_order.assign(d, 0);
+  for (int i = 0; i < d; ++i) e->draw_order[i] = i;
+  switch (p->kind) {
+    case PBH_PROP_GAUSS: {
+      if (!p->loc || !p->scale) return fail(PBH_ERR_ARG, "GAUSS needs loc, scale");
+      oloc = pack(blk, p->loc, d);
+      oscl = pack(blk, p->scale, d);
+      if (p->order) {
+        std::vector<int> seen(d, 0);
+        for (int j = 0; j < d; ++j) {
+          const int k = p->order[j];
+          if (k < 0 || k >= d || seen[k]++)
+            return fail(PBH_ERR_ARG, "order must be a permutation of 0..%d", d - 1);
+          e->draw_order[j] = k;
+        }
+      }
+      break;
+    }
+    case PBH_PROP_SPHERE:
+      if (!p->lengths) return fail(PBH_ERR_ARG, "SPHERE needs lengths");
+      olen = pack(blk, p->lengths, d);
+      break;
+    case PBH_PROP_UNIFORM:
+      if (!p->delta_vec) return fail(PBH_ERR_ARG, "UNIFORM needs delta_vec");
+      odel = pack(blk, p->delta_vec, d);
+      break;
+    default:
+      return fail(PBH_ERR_ARG, "bad proposal kind %d (GIBBS: pbh_set_gibbs)", p->kind);
+  }
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = upload(e->dprop, blk, e->stream);
+  if (rc) return rc;
+  KArgs &k = e->k;
+  k.prop = p->kind;
+  k.ploc = e->dprop + oloc; k.pscl = e->dprop + oscl;
+  k.plen = e->dprop + olen; k.pdel = e->dprop + odel;
+  k.sdelta = p->delta;
+  e->has_prop = true;
+  e->has_gibbs = false;
+  return PBH_OK;
+}
+
+int pbh_set_gibbs(pbh_engine *e, const pbh_gibbs *gb) {
+  if (check_ptr(e, "engine") || check_ptr(gb, "gibbs")) return PBH_ERR_ARG;
+  if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
+  if (e->k.target != PBH_TARGET_MVN || e->k.scores != PBH_SCORES_GIBBS)
+    return fail(PBH_ERR_UNSUPPORTED,
+                "CondCov Gibbs needs an MVN target and gibbs scores");
+  const int d = e->d;
+  if (!gb->mean || !gb->stdv || !gb->cdf || (d > 1 && !gb->coef))
+    return fail(PBH_ERR_ARG, "gibbs tables missing");
+  if (gb->tsteps < 1 || gb->tsteps > d)
+    return fail(PBH_ERR_ARG, "tsteps %d outside 1..%d", gb->tsteps, d);
+  std::vector<double> blk;
+  const size_t om = pack(blk, gb->mean, d);
+  const size_t oc = pack(blk, gb->coef ? gb->coef : gb->mean, d > 1 ? (int64_t)d * (d - 1) : 0);
+  const size_t os = pack(blk, gb->stdv, d);
+  const size_t ocdf = pack(blk, gb->cdf, 2 * d);
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = upload(e->dgibbs, blk, e->stream);
+  if (rc) return rc;
+  KArgs &k = e->k;
+  k.gmean = e->dgibbs + om; k.gcoef = e->dgibbs + oc;
+  k.gstdv = e->dgibbs + os; k.gcdf = e->dgibbs + ocdf;
+  k.tsteps = gb->tsteps;
+  k.prop = PBH_PROP_GIBBS;
+  e->draw_order.assign(gb->tsteps, 0);
+  for (int i = 0; i < gb->tsteps; ++i) e->draw_order[i] = i;
+  e->has_gibbs = true;
+  e->has_prop = false;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// chains, randomness
+// ---------------------------------------------------------------------------
+int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
+  if (check_ptr(e, "engine") || check_ptr(init, "init")) return PBH_ERR_ARG;
+  if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
+  if (n < 1 || off < 0) return fail(PBH_ERR_ARG, "bad n_chains/offset");
+  const int d = e->d;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (n != e->n) {
+    free_trace(e);
+    int rc = dalloc(e->x, (size_t)n * d);
+    if (!rc) rc = dalloc(e->lp, n);
+    if (!rc) rc = dalloc(e->msum, (size_t)n * d);
+    if (!rc) rc = dalloc(e->msq, (size_t)n * d);
+    if (!rc) rc = dalloc(e->nacc, n);
+    if (rc) return rc;
+  }
+  std::vector<double> xt((size_t)n * d);
+  for (int64_t c = 0; c < n; ++c)
+    for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = init[(size_t)c * d + k];
+  HIP_TRY(hipMemcpy(e->x, xt.data(), xt.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(e->lp, 0, n * sizeof(double)));
+  HIP_TRY(hipMemset(e->msum, 0, (size_t)n * d * sizeof(double)));
+  HIP_TRY(hipMemset(e->msq, 0, (size_t)n * d * sizeof(double)));
+  HIP_TRY(hipMemset(e->nacc, 0, n * sizeof(int64_t)));
+  e->n = n;
+  e->off = off;
+  e->has_pred = false;
+  e->g = 0;
+  e->mom_steps = 0;
+  e->rec_base = 0;
+  dfree(e->rep);
+  e->rep_steps = 0;
+  e->rep_g0 = 0;
+  return PBH_OK;
+}
+
+int pbh_set_rng(pbh_engine *e, int32_t mode, uint64_t seed) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX)
+    return fail(PBH_ERR_ARG, "bad rng mode %d", mode);
+  e->rng = mode;
+  e->seed = seed;
+  return PBH_OK;
+}
+
+int pbh_stream_width(pbh_engine *e, int32_t *r) {
+  if (check_ptr(e, "engine") || check_ptr(r, "r")) return PBH_ERR_ARG;
+  if (e->has_gibbs) *r = e->k.tsteps;
+  else if (e->has_prop) *r = e->d + 1;
+  else return fail(PBH_ERR_STATE, "no proposal or gibbs tables set");
+  return PBH_OK;
+}
+
+int pbh_upload_replay(pbh_engine *e, int64_t n_steps, const double *rand) {
+  if (check_ptr(e, "engine") || check_ptr(rand, "rand")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  int32_t R = 0;
+  int rc = pbh_stream_width(e, &R);
+  if (rc) return rc;
+  if (n_steps < 1) return fail(PBH_ERR_ARG, "n_steps must be >= 1");
+  const int64_t n = e->n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  rc = dalloc(e->rep, (size_t)n_steps * R * n);
+  if (rc) return rc;
+  // Reorder draws so that device row k feeds dim k (GAUSS Delta keyword
+  // order); the threshold row (index d for MH) stays last.
+  std::vector<double> row((size_t)R * n);
+  for (int64_t t = 0; t < n_steps; ++t) {
+    const double *src = rand + (size_t)t * R * n;
+    for (int j = 0; j < R; ++j) {
+      const int dst = j < (int)e->draw_order.size() ? e->draw_order[j] : j;
+      std::memcpy(&row[(size_t)dst * n], src + (size_t)j * n, n * sizeof(double));
+    }
+    HIP_TRY(hipMemcpy(e->rep + (size_t)t * R * n, row.data(),
+                      row.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  e->k.R = R;
+  e->rep_steps = n_steps;
+  e->rep_g0 = e->g;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// running
+// ---------------------------------------------------------------------------
+int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  if (capacity < 0 || thin < 1) return fail(PBH_ERR_ARG, "bad capacity/thin");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  free_trace(e);
+  const int64_t n = e->n, d = e->d, W = (n + 63) / 64;
+  int rc = PBH_OK;
+  if (capacity > 0) {
+    rc = dalloc(e->tx, (size_t)capacity * d * n);
+    if (!rc) rc = dalloc(e->tlp, (size_t)capacity * n);
+    if (!rc) rc = dalloc(e->tacc, (size_t)capacity * W);
+    if (!rc && debug) {
+      rc = dalloc(e->tpx, (size_t)capacity * d * n);
+      if (!rc) rc = dalloc(e->tpp, (size_t)capacity * n);
+      if (!rc) rc = dalloc(e->ts, (size_t)capacity * n);
+    }
+  }
+  if (rc) {
+    free_trace(e);
+    return rc;
+  }
+  e->cap = capacity;
+  e->thin = thin;
+  e->debug = debug ? 1 : 0;
+  e->rec_base = e->g / thin;
+  return PBH_OK;
+}
+
+int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->has_model || (!e->has_prop && !e->has_gibbs))
+    return fail(PBH_ERR_STATE, "model and proposal/gibbs tables must be set");
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  if (e->has_gibbs != (e->k.scores == PBH_SCORES_GIBBS))
+    return fail(PBH_ERR_STATE, "gibbs scores need gibbs tables and vice versa");
+  if (n_steps < 0) return fail(PBH_ERR_ARG, "n_steps < 0");
+  if (n_steps == 0) {
+    e->timed = false;
+    e->last_launches = 0;
+    return PBH_OK;
+  }
+  if (e->rng == PBH_RNG_REPLAY &&
+      (!e->rep || e->g < e->rep_g0 || e->g + n_steps > e->rep_g0 + e->rep_steps))
+    return fail(PBH_ERR_STATE,
+                "replay stream covers steps [%lld, %lld), run needs [%lld, %lld)",
+                (long long)e->rep_g0, (long long)(e->rep_g0 + e->rep_steps),
+                (long long)e->g, (long long)(e->g + n_steps));
+  if (e->cap > 0) {
+    const int64_t recs = (e->g + n_steps) / e->thin - e->rec_base;
+    if (recs > e->cap)
+      return fail(PBH_ERR_STATE, "trace capacity %lld < %lld records",
+                  (long long)e->cap, (long long)recs);
+  }
+  HIP_TRY(hipSetDevice(e->device));
+  const int64_t spl = steps_per_launch > 0 ? steps_per_launch : n_steps;
+  KArgs k = e->k;
+  k.n = e->n;
+  k.off = e->off;
+  k.x = e->x;
+  k.lp = e->lp;
+  k.rng = e->rng;
+  k.seed_lo = (uint32_t)e->seed;
+  k.seed_hi = (uint32_t)(e->seed >> 32);
+  k.rep = e->rep;
+  k.tx = e->tx; k.tlp = e->tlp; k.tpx = e->tpx; k.tpp = e->tpp; k.ts = e->ts;
+  k.tacc = e->tacc;
+  k.thin = e->cap > 0 ? e->thin : 1;
+  k.rec_base = e->rec_base;
+  k.rec_cap = e->cap;
+  k.debug = e->debug;
+  k.W = (e->n + 63) / 64;
+  k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
+  const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384)
+                         ? (size_t)k.tn * sizeof(double) : 0;
+  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  int64_t launches = 0;
+  for (int64_t done = 0; done < n_steps;) {
+    const int64_t m = std::min(spl, n_steps - done);
+    k.n_steps = (int32_t)m;
+    k.g0 = e->g;
+    k.has_pred = e->has_pred ? 1 : 0;
+    k.rep_row0 = e->g - e->rep_g0;
+    hipError_t err = e->has_gibbs ? pbh::launch_gibbs(k, e->stream)
+                                  : pbh::launch_mh(k, e->stream, lds);
+    if (err != hipSuccess)
+      return fail(PBH_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(err));
+    e->g += m;
+    e->has_pred = true;
+    done += m;
+    ++launches;
+  }
+  HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->mom_steps += n_steps;
+  e->timed = true;
+  e->last_launches = launches;
+  return PBH_OK;
+}
+
+int pbh_sync(pbh_engine *e) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return PBH_OK;
+}
+
+int pbh_last_run_ms(pbh_engine *e, double *ms, int64_t *launches) {
+  if (check_ptr(e, "engine") || check_ptr(ms, "ms")) return PBH_ERR_ARG;
+  if (!e->timed) {
+    *ms = 0.;
+    if (launches) *launches = 0;
+    return PBH_OK;
+  }
+  HIP_TRY(hipEventSynchronize(e->ev1));
+  float f = 0.f;
+  HIP_TRY(hipEventElapsedTime(&f, e->ev0, e->ev1));
+  *ms = f;
+  if (launches) *launches = e->last_launches;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// results
+// ---------------------------------------------------------------------------
+int pbh_get_state(pbh_engine *e, double *x, double *logp) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const int64_t n = e->n;
+  const int d = e->d;
+  if (x) {
+    std::vector<double> xt((size_t)n * d);
+    HIP_TRY(hipMemcpy(xt.data(), e->x, xt.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t c = 0; c < n; ++c)
+      for (int k = 0; k < d; ++k) x[(size_t)c * d + k] = xt[(size_t)k * n + c];
+  }
+  if (logp) HIP_TRY(hipMemcpy(logp, e->lp, n * sizeof(double), hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_trace_len(pbh_engine *e, int64_t *n_recorded) {
+  if (check_ptr(e, "engine") || check_ptr(n_recorded, "n_recorded")) return PBH_ERR_ARG;
+  const int64_t r = e->cap > 0 ? e->g / e->thin - e->rec_base : 0;
+  *n_recorded = std::max<int64_t>(0, std::min(r, e->cap));
+  return PBH_OK;
+}
+
+int pbh_get_trace(pbh_engine *e, int64_t first, int64_t cnt, double *x,
+                  double *logp, uint64_t *acc, double *p_x, double *p_p,
+                  double *s) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  int64_t rec = 0;
+  pbh_trace_len(e, &rec);
+  if (first < 0 || cnt < 0 || first + cnt > rec)
+    return fail(PBH_ERR_ARG, "trace range [%lld, %lld) outside [0, %lld)",
+                (long long)first, (long long)(first + cnt), (long long)rec);
+  if ((p_x || p_p || s) && !e->debug)
+    return fail(PBH_ERR_STATE, "debug trace not allocated");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const size_t n = e->n, d = e->d, W = (e->n + 63) / 64;
+  if (cnt == 0) return PBH_OK;
+  if (x) HIP_TRY(hipMemcpy(x, e->tx + first * d * n, cnt * d * n * sizeof(double), hipMemcpyDeviceToHost));
+  if (logp) HIP_TRY(hipMemcpy(logp, e->tlp + first * n, cnt * n * sizeof(double), hipMemcpyDeviceToHost));
+  if (acc) HIP_TRY(hipMemcpy(acc, e->tacc + first * W, cnt * W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (p_x) HIP_TRY(hipMemcpy(p_x, e->tpx + first * d * n, cnt * d * n * sizeof(double), hipMemcpyDeviceToHost));
+  if (p_p) HIP_TRY(hipMemcpy(p_p, e->tpp + first * n, cnt * n * sizeof(double), hipMemcpyDeviceToHost));
+  if (s) HIP_TRY(hipMemcpy(s, e->ts + first * n, cnt * n * sizeof(double), hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_get_moments(pbh_engine *e, double *sum, double *sumsq, int64_t *n_acc,
+                    int64_t *n_steps) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const size_t dn = (size_t)e->d * e->n;
+  if (sum) HIP_TRY(hipMemcpy(sum, e->msum, dn * sizeof(double), hipMemcpyDeviceToHost));
+  if (sumsq) HIP_TRY(hipMemcpy(sumsq, e->msq, dn * sizeof(double), hipMemcpyDeviceToHost));
+  if (n_acc) HIP_TRY(hipMemcpy(n_acc, e->nacc, e->n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (n_steps) *n_steps = e->mom_steps;
+  return PBH_OK;
+}
+
+int pbh_reset_moments(pbh_engine *e) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  HIP_TRY(hipSetDevice(e->device));
+  const size_t dn = (size_t)e->d * e->n;
+  HIP_TRY(hipMemsetAsync(e->msum, 0, dn * sizeof(double), e->stream));
+  HIP_TRY(hipMemsetAsync(e->msq, 0, dn * sizeof(double), e->stream));
+  HIP_TRY(hipMemsetAsync(e->nacc, 0, e->n * sizeof(int64_t), e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->mom_steps = 0;
+  return PBH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL
+// ---------------------------------------------------------------------------
+int pbh_rccl_unique_id(uint8_t id[128]) {
+  if (check_ptr(id, "id")) return PBH_ERR_ARG;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId uid;
+  RCCL_TRY(ncclGetUniqueId(&uid));
+  std::memcpy(id, &uid, 128);
+  return PBH_OK;
+}
+
+int pbh_rccl_init(pbh_engine *e, int32_t rank, int32_t world, const uint8_t id[128]) {
+  if (check_ptr(e, "engine") || check_ptr(id, "id")) return PBH_ERR_ARG;
+  if (world < 1 || rank < 0 || rank >= world) return fail(PBH_ERR_ARG, "bad rank/world");
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->comm) {
+    ncclCommDestroy(e->comm);
+    e->comm = nullptr;
+  }
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  RCCL_TRY(ncclCommInitRank(&e->comm, world, uid, rank));
+  e->rank = rank;
+  e->world = world;
+  return PBH_OK;
+}
+
+int pbh_rccl_allgather_moments(pbh_engine *e, double *out) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  HIP_TRY(hipSetDevice(e->device));
+  const int64_t n = e->n, dn = (int64_t)e->d * n, cnt = 2 * dn + n;
+  int rc = dalloc(e->gather_send, cnt);
+  if (!rc) rc = dalloc(e->gather_recv, (size_t)cnt * e->world);
+  if (rc) return rc;
+  const int64_t m = std::max(dn, n);
+  hipLaunchKernelGGL(pack_moments, dim3((unsigned)((m + 255) / 256)), dim3(256),
+                     0, e->stream, e->msum, e->msq, e->nacc, e->gather_send, dn, n);
+  HIP_TRY(hipGetLastError());
+  RCCL_TRY(ncclAllGather(e->gather_send, e->gather_recv, (size_t)cnt,
+                         ncclFloat64, e->comm, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(out, e->gather_recv, (size_t)cnt * e->world * sizeof(double),
+                    hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
+  if (check_ptr(e, "engine") || check_ptr(value, "value")) return PBH_ERR_ARG;
+  if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = e->scalar ? PBH_OK : dalloc(e->scalar, 1);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(e->scalar, value, sizeof(double), hipMemcpyHostToDevice));
+  RCCL_TRY(ncclAllReduce(e->scalar, e->scalar, 1, ncclFloat64, ncclMax, e->comm,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(value, e->scalar, sizeof(double), hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_rccl_destroy(pbh_engine *e) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (e->comm) {
+    HIP_TRY(hipSetDevice(e->device));
+    RCCL_TRY(ncclCommDestroy(e->comm));
+    e->comm = nullptr;
+  }
+  return PBH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// pbh_kernels.h -- kernel argument block shared by the engine (host) and the
+// gfx950 kernels.  Passed by value as the kernarg segment; every pointer in it
+// is a device pointer and every array read through it is read with a
+// wave-uniform address (scalar loads).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbh {
+
+struct KArgs {
+  // ---- model (pbh_model) ----
+  int32_t d, target, pscale, scores;
+  const double *ta, *tb, *tc, *te;  // target parameter arrays (see pbhip.h)
+  int64_t tn;                       // n_obs (NORM_IID) or K (GMM)
+  int32_t i0, i1;                   // NORM_IID loc / scale dims
+  int32_t has_prior;
+  const double *plo, *phi;
+  uint32_t plo_incl, phi_incl;      // bitmasks over dims
+  double prior_logp;
+  uint32_t ufun;                    // bitmask: dim uses the (log, exp) ufun
+  int32_t tran_kind, tran_sym, tran_rev;  // tran_rev: product order reversed
+  double tran_value, tran_scale;
+  const double *tran_off;
+  // ---- proposal ----
+  int32_t prop;
+  const double *ploc, *pscl, *plen, *pdel;
+  double sdelta;
+  // ---- gibbs ----
+  const double *gmean, *gcoef, *gstdv, *gcdf;
+  int32_t tsteps;
+  // ---- host-evaluated constants (bit-identical to the reference's) ----
+  double log_npi;    // np.log(NEARLY_POSITIVE_INF)
+  double norm_logC;  // np.log(np.sqrt(2*np.pi))
+  double norm_C;     // np.sqrt(2*np.pi)
+  // ---- run ----
+  int64_t n;         // chains on this engine
+  int64_t off;       // global id of chain 0 (Philox key input)
+  int32_t n_steps;   // steps in this launch
+  int64_t g0;        // global step index of the launch's first step
+  int32_t has_pred;  // chains already hold an accepted pred (step > 1)
+  double *x;         // state [d][n]
+  double *lp;        // log/lin prob of the state [n]
+  int32_t rng;       // PBH_RNG_*
+  uint32_t seed_lo, seed_hi;
+  const double *rep; // replay stream [T][R][n]
+  int64_t rep_row0;  // replay step index of g0
+  int32_t R;         // replay draws per step
+  // ---- trace ----
+  double *tx, *tlp, *tpx, *tpp, *ts;
+  uint64_t *tacc;
+  int32_t thin;
+  int64_t rec_base;  // records made before the trace buffer was allocated
+  int64_t rec_cap;
+  int32_t debug;
+  int64_t W;         // accept-mask words per recorded step = ceil(n / 64)
+  // ---- moments ----
+  double *msum, *msq;
+  int64_t *nacc;
+};
+
+// Host launchers (pbh_kernels.hip).
+hipError_t launch_mh(const KArgs &a, hipStream_t s, size_t lds_bytes);
+hipError_t launch_gibbs(const KArgs &a, hipStream_t s);
+bool mh_dim_supported(int d);
+
+}  // namespace pbh

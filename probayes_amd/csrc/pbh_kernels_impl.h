@@ -1,0 +1,494 @@
+// pbh_kernels_impl.h -- gfx950 kernels of the batched MH / CondCov-Gibbs engine.
+//
+// Layout and mapping: one chain per lane, 64 chains per
+// wavefront, the chain state x[d] and running moments live in VGPRs for the
+// whole fused step loop; every HBM access is chain-contiguous
+// ([step][dim][chain]) so a wavefront moves 512 contiguous bytes per fp64
+// load/store.  Model constants are read with wave-uniform addresses (scalar
+// loads), NORM_IID observations are staged once per workgroup in LDS.
+//
+// One chain-step restates SP.next (sp.py:221-258):
+//   draws -> delta (field.py:469-531 / variable.py:600-638 / callable Delta)
+//   -> x' = x + delta or exp(log x + delta)   (variable.py:641-697)
+//   -> joint density (rf.py:565-581, sd.py:148-161, rv_utils.py:8-47)
+//   -> score (sp_utils.py:19-64) -> s >= t (sp_utils.py:34-37)
+//   -> keep (x', p') on accept else (x, p)  (sp.py:253-256)
+#pragma once
+#include "pbh_kernels.h"
+#include "pbh_device.h"
+#include "../../include/pbhip.h"
+
+namespace pbh {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// prob.py:354-357: the mvn density is evaluated at the values reversed and,
+// for d > 2, rotated by one: [x_{d-2}, ..., x_0, x_{d-1}] (App. A-4).
+template <int D>
+__device__ __forceinline__ constexpr int mvn_perm(int i) {
+  return D <= 1 ? 0 : (D == 2 ? 1 - i : (i < D - 1 ? D - 2 - i : D - 1));
+}
+
+// scipy norm.logpdf(x, loc, scale): _norm_logpdf((x - loc) / scale) -
+// log(scale), _norm_logpdf(y) = -y**2 / 2.0 - _norm_pdf_logC.
+__device__ __forceinline__ double norm_logpdf(double x, double loc,
+                                              double scale, double logscale,
+                                              double logC) {
+  const double y = (x - loc) / scale;
+  return ((-(y * y)) / 2.0 - logC) - logscale;
+}
+
+// scipy norm.pdf: np.exp(-y**2 / 2.0) / _norm_pdf_C / scale.
+__device__ __forceinline__ double norm_pdf(double x, double loc, double scale,
+                                           double C) {
+  const double y = (x - loc) / scale;
+  return (exp((-(y * y)) / 2.0) / C) / scale;
+}
+
+// scipy uniform.pdf: 1.0 / scale on the closed support [loc, loc + scale].
+__device__ __forceinline__ double uniform_pdf(double x, double lo,
+                                              double scale) {
+  const double y = (x - lo) / scale;
+  return (0.0 <= y && y <= 1.0) ? 1.0 / scale : 0.0;
+}
+
+__device__ __forceinline__ u32x4 ctr(uint32_t j, int64_t g, int64_t chain) {
+  return u32x4{j, (uint32_t)g, (uint32_t)chain,
+               (uint32_t)((uint64_t)chain >> 32) ^
+                   ((uint32_t)((uint64_t)g >> 32) << 16)};
+}
+
+// ---------------------------------------------------------------------------
+// Joint density of x' (in the pscale of the model)
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ double mvn_density(const KArgs &a,
+                                              const double (&x)[D]) {
+  // scipy _PSD form: maha = sum(square(dev . prec_U)); logpdf =
+  // -0.5 * (rank*log(2pi) + log_pdet + maha); pdf = exp(logpdf).
+  double dev[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) dev[i] = x[mvn_perm<D>(i)] - a.ta[i];
+  double sq[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double y = dev[0] * a.tb[j];
+#pragma unroll
+    for (int i = 1; i < D; ++i) y = y + dev[i] * a.tb[i * D + j];
+    sq[j] = y * y;
+  }
+  const double maha = np_sum_regs<D>(sq, D);
+  const double logpdf = -0.5 * (a.tc[0] + maha);
+  return a.pscale == PBH_PSCALE_LIN ? exp(logpdf) : logpdf;
+}
+
+template <int D>
+__device__ __forceinline__ double joint_density(const KArgs &a,
+                                                const double (&x)[D],
+                                                const double *obs_lds,
+                                                bool use_lds) {
+  double out = 0.0;
+  switch (a.target) {
+    case PBH_TARGET_DIAG_GAUSS: {
+      // lp(**kw) = sum(norm.logpdf(kw[k], mu_k, sigma_k)): Python sum from 0
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        out = out + norm_logpdf(x[k], a.ta[k], a.tb[k], a.tc[k], a.norm_logC);
+      break;
+    }
+    case PBH_TARGET_NORM_IID: {
+      double mu = 0., sg = 1.;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        if (k == a.i0) mu = x[k];
+        if (k == a.i1) sg = x[k];
+      }
+      const double lsg = log(sg);
+      const double logC = a.norm_logC;
+      if (use_lds) {
+        out = np_pairwise(
+            [&](int64_t j) { return norm_logpdf(obs_lds[j], mu, sg, lsg, logC); },
+            a.tn);
+      } else {
+        const double *obs = a.ta;
+        out = np_pairwise(
+            [&](int64_t j) { return norm_logpdf(obs[j], mu, sg, lsg, logC); },
+            a.tn);
+      }
+      break;
+    }
+    case PBH_TARGET_GMM: {
+      // a_k = logw_k + sum_i logpdf(x_i, mu_ki, sd_k); m + log(sum exp(a - m))
+      const int64_t K = a.tn;
+      auto comp = [&](int64_t k) {
+        double v = a.ta[k];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+          v = v + norm_logpdf(x[i], a.tb[k * D + i], a.tc[k], a.te[k],
+                              a.norm_logC);
+        return v;
+      };
+      double m = comp(0);
+      for (int64_t k = 1; k < K; ++k) {
+        const double v = comp(k);
+        m = (m != m) ? m : ((v != v || v > m) ? v : m);  // np.max: NaN wins
+      }
+      const double s = np_pairwise([&](int64_t k) { return exp(comp(k) - m); }, K);
+      out = m + log(s);
+      break;
+    }
+    case PBH_TARGET_NORM_PDF: {
+      out = norm_pdf(x[0], a.ta[0], a.tb[0], a.norm_C);
+#pragma unroll
+      for (int k = 1; k < D; ++k)
+        out = out * norm_pdf(x[k], a.ta[k], a.tb[k], a.norm_C);
+      break;
+    }
+    case PBH_TARGET_UNIFORM_PDF: {
+      out = uniform_pdf(x[0], a.ta[0], a.tb[0]);
+#pragma unroll
+      for (int k = 1; k < D; ++k) out = out * uniform_pdf(x[k], a.ta[k], a.tb[k]);
+      break;
+    }
+    case PBH_TARGET_MVN:
+      out = mvn_density<D>(a, x);
+      break;
+    default:
+      out = __builtin_nan("");
+  }
+  if (a.has_prior) {
+    // rv_prod_rule of the roots' uniform_prob (rf_utils.py:10-42,
+    // rv_utils.py:30-38), then product(cond, dist) (sd.py:158-161)
+    bool inside = true;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const bool lo_ok = ((a.plo_incl >> k) & 1u) ? (x[k] >= a.plo[k])
+                                                   : (x[k] > a.plo[k]);
+      const bool hi_ok = ((a.phi_incl >> k) & 1u) ? (x[k] <= a.phi[k])
+                                                   : (x[k] < a.phi[k]);
+      inside = inside && lo_ok && hi_ok;
+    }
+    out = (inside ? a.prior_logp : kNearlyNegInf) + out;
+  }
+  return out;
+}
+
+// pscales.py:219-236 div_prob(a, b, pscale, pscale, pscale=1.)
+__device__ __forceinline__ double div_prob(const KArgs &a, double num,
+                                           double den) {
+  const bool lin = a.pscale == PBH_PSCALE_LIN;
+  const double A = lin ? num : exp_logp(num, a.log_npi);
+  const double B = lin ? den : exp_logp(den, a.log_npi);
+  return A / np_max_tiny(B);
+}
+
+// hastings_scores / metropolis_scores (sp_utils.py:19-64).  Returns false
+// when the score is None (auto-accept), else writes s.
+template <int D>
+__device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
+                                      const double (&xp)[D], double lp,
+                                      double lpp, double &s) {
+  if (a.scores == PBH_SCORES_METROPOLIS) {
+    const double q = div_prob(a, lpp, lp);
+    s = q < 1. ? q : 1.;  // Python min(1., q)
+    return true;
+  }
+  double q;
+  if (a.tran_kind == PBH_TRAN_CONST) {
+    q = a.tran_value;
+  } else {
+    // prod of norm.pdf(x'_k, x_k + off_k, scale) in the callable's order
+    q = 1.0;
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int k = a.tran_rev ? (D - 1 - j) : j;
+      double v = 0.;
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk)
+        if (kk == k) v = norm_pdf(xp[kk], x[kk] + a.tran_off[kk], a.tran_scale, a.norm_C);
+      q = first ? v : q * v;
+      first = false;
+    }
+  }
+  // rescale(q, pscale, 1.) (pscales.py:100-131)
+  const double qt = a.pscale == PBH_PSCALE_LIN ? q : exp_logp(q, a.log_npi);
+  if (qt <= 0.) return false;                      // sp_utils.py:53-54
+  double r;
+  if (a.tran_sym) {
+    r = div_prob(a, lpp, lp);                      // :56
+  } else {
+    // reval_tran returns the forward value (rf.py:536): r~ == q~
+    r = div_prob(a, lpp * qt, lp * qt);            // :62-64
+  }
+  s = r < 1. ? r : 1.;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// MH kernel: n_steps fused chain-steps, one chain per lane
+// ---------------------------------------------------------------------------
+template <int D, int RNG>
+__global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
+  extern __shared__ double s_obs[];
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int lane = threadIdx.x & 63;
+
+  bool use_lds = false;
+  if (a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
+    for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = a.ta[j];
+    __syncthreads();
+    use_lds = true;
+  }
+
+  double x[D], ms[D], mq[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    x[k] = a.x[k * a.n + cc];
+    ms[k] = 0.;
+    mq[k] = 0.;
+  }
+  double lp = a.lp[cc];
+  int64_t nacc = 0;
+  const int64_t chain = a.off + cc;
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const int64_t g = a.g0 + s;
+    // ---- draws ----
+    double r[D];
+    double thr;
+    if (RNG == PBH_RNG_REPLAY) {
+      const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
+#pragma unroll
+      for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
+      thr = row[(int64_t)D * a.n];
+    } else {
+      if (a.prop == PBH_PROP_GAUSS) {
+#pragma unroll
+        for (int p = 0; p < (D + 1) / 2; ++p) {
+          double z0, z1;
+          box_muller(philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi), z0, z1);
+          r[2 * p] = z0;
+          if (2 * p + 1 < D) r[2 * p + 1] = z1;
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < (D + 1) / 2; ++p) {
+          const u32x4 w = philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi);
+          r[2 * p] = u01(w.x, w.y);
+          if (2 * p + 1 < D) r[2 * p + 1] = u01(w.z, w.w);
+        }
+      }
+      const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+      thr = u01(w.x, w.y);
+    }
+    // ---- proposal ----
+    double xp[D];
+    {
+      double dl[D];
+      if (a.prop == PBH_PROP_GAUSS) {
+        // scipy rv_generic.rvs: z * scale + loc
+#pragma unroll
+        for (int k = 0; k < D; ++k) dl[k] = r[k] * a.pscl[k] + a.ploc[k];
+      } else if (a.prop == PBH_PROP_UNIFORM) {
+        // np.random.uniform(-delta, delta) = low + (high - low) * u
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double d0 = a.pdel[k];
+          dl[k] = -d0 + (d0 - -d0) * r[k];
+        }
+      } else {
+        // spherical tuple delta (field.py:509-531)
+        const double d0 = a.sdelta;
+        double sq[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          dl[k] = -d0 + (d0 - -d0) * r[k];
+          sq[k] = dl[k] * dl[k];
+        }
+        const double ss = np_sum_regs<D>(sq, D);
+        const double rss = ss >= kNearlyPosZero ? sqrt(ss) : 0.;
+#pragma unroll
+        for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * a.plen[k];
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        xp[k] = ((a.ufun >> k) & 1u) ? exp(log(x[k]) + dl[k]) : x[k] + dl[k];
+    }
+    // ---- density, score, accept ----
+    const double lpp = joint_density<D>(a, xp, s_obs, use_lds);
+    double sc = __builtin_nan("");
+    bool acc;
+    if (!a.has_pred && s == 0) {
+      acc = true;                                  // s = None on step 1
+    } else {
+      acc = !score<D>(a, x, xp, lp, lpp, sc) || (sc >= thr);
+    }
+    if (acc) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = xp[k];
+      lp = lpp;
+    }
+    nacc += acc ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      ms[k] += x[k];
+      mq[k] += x[k] * x[k];
+    }
+    // ---- trace (every thin-th step, wave-uniform condition) ----
+    if ((g + 1) % a.thin == 0) {
+      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+      if (rec >= 0 && rec < a.rec_cap) {
+        if (active) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) a.tx[(rec * D + k) * a.n + c] = x[k];
+          a.tlp[rec * a.n + c] = lp;
+          if (a.debug) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) a.tpx[(rec * D + k) * a.n + c] = xp[k];
+            a.tpp[rec * a.n + c] = lpp;
+            a.ts[rec * a.n + c] = sc;
+          }
+        }
+        const uint64_t mask = __ballot(active && acc);
+        const int64_t wv = c >> 6;
+        if (lane == 0 && wv < a.W) a.tacc[rec * a.W + wv] = mask;
+      }
+    }
+  }
+
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      a.x[k * a.n + c] = x[k];
+      a.msum[k * a.n + c] += ms[k];
+      a.msq[k * a.n + c] += mq[k];
+    }
+    a.lp[c] = lp;
+    a.nacc[c] += nacc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CondCov Gibbs kernel (cond_cov.py:42-65 per coordinate; rf.py:446-458
+// cycling).  One SP step updates tsteps coordinates; u is always True.
+// ---------------------------------------------------------------------------
+template <int D, int RNG>
+__global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int lane = threadIdx.x & 63;
+  double x[D], ms[D], mq[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    x[k] = a.x[k * a.n + cc];
+    ms[k] = 0.;
+    mq[k] = 0.;
+  }
+  double lp = a.lp[cc];
+  const int64_t chain = a.off + cc;
+  const int ts = a.tsteps;
+  const int nblk = (D + ts - 1) / ts;
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const int64_t g = a.g0 + s;
+    const int cm = (int)(g % nblk) * ts;
+    int j = 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      if (k >= cm && k < cm + ts) {
+        double u;
+        if (RNG == PBH_RNG_REPLAY) {
+          u = a.rep[((a.rep_row0 + s) * a.R + j) * a.n + cc];
+        } else {
+          const u32x4 w = philox4x32_10(ctr(j, g, chain), a.seed_lo, a.seed_hi);
+          u = u01(w.x, w.y);
+        }
+        ++j;
+        // mean + coef_k . (x_{-k} - mu_{-k})
+        double dot = 0.;
+        bool first = true;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          if (i == k) continue;
+          const int jj = i < k ? i : i - 1;
+          const double t = a.gcoef[k * (D - 1) + jj] * (x[i] - a.gmean[i]);
+          dot = first ? t : dot + t;
+          first = false;
+        }
+        const double lo = a.gcdf[2 * k], hi = a.gcdf[2 * k + 1];
+        const double cdf = lo + (hi - lo) * u;     // np.random.uniform(lo, hi)
+        const double m = a.gmean[k] + dot;
+        x[k] = ndtri(cdf) * a.gstdv[k] + m;        // norm.ppf(cdf, m, sd)
+      }
+    }
+    lp = mvn_density<D>(a, x);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      ms[k] += x[k];
+      mq[k] += x[k] * x[k];
+    }
+    if ((g + 1) % a.thin == 0) {
+      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+      if (rec >= 0 && rec < a.rec_cap) {
+        if (active) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) a.tx[(rec * D + k) * a.n + c] = x[k];
+          a.tlp[rec * a.n + c] = lp;
+          if (a.debug) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) a.tpx[(rec * D + k) * a.n + c] = x[k];
+            a.tpp[rec * a.n + c] = lp;
+            a.ts[rec * a.n + c] = __builtin_nan("");
+          }
+        }
+        const uint64_t mask = __ballot(active);
+        const int64_t wv = c >> 6;
+        if (lane == 0 && wv < a.W) a.tacc[rec * a.W + wv] = mask;
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      a.x[k * a.n + c] = x[k];
+      a.msum[k * a.n + c] += ms[k];
+      a.msq[k * a.n + c] += mq[k];
+    }
+    a.lp[c] = lp;
+    a.nacc[c] += a.n_steps;
+  }
+}
+
+}  // namespace
+
+template <int D>
+hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
+  const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
+  if (a.rng == PBH_RNG_REPLAY)
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_REPLAY>), grid, block, lds, st, a);
+  else
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX>), grid, block, lds, st, a);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
+  if (a.rng == PBH_RNG_REPLAY)
+    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX>), grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
+#define PBH_INSTANTIATE(D)                                                  \
+  template hipError_t launch_mh_d<D>(const KArgs &, hipStream_t, size_t); \
+  template hipError_t launch_gibbs_d<D>(const KArgs &, hipStream_t);
+
+}  // namespace pbh

@@ -1,0 +1,308 @@
+"""Engine: a spec (probayes_amd/spec.py) bound to one libpbhip engine/device.
+
+Host-side precompute mirrors what the reference evaluates with NumPy/SciPy
+once per model, so the device sees bit-identical constants:
+  * log(scale) of every Normal (scipy norm.logpdf, _distn_infrastructure.py);
+  * the mvn whitening matrix, log_pdet and rank of scipy's CovViaPSD
+    (prob.py:349-358 -> multivariate_normal.pdf);
+  * the CondCov tables coef / stdv / cdf limits (cond_cov.py:22-39).
+Everything per chain-step runs in the HIP kernels; nothing here loops over
+chains or steps.
+"""
+import ctypes
+
+import numpy as np
+import scipy.stats
+
+from probayes_amd import _lib
+from probayes_amd.spec import normalize_spec
+
+_c = ctypes
+
+
+def _dp(a):
+  return a.ctypes.data_as(_c.POINTER(_c.c_double))
+
+
+def _ip(a):
+  return a.ctypes.data_as(_c.POINTER(_c.c_int32))
+
+
+def _f64(a):
+  return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a):
+  return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def condcov_tables(mean, cov, lo, hi):
+  """CondCov.__init__ (cond_cov.py:22-39): per coordinate i the regression
+  row Sigma_{i,-i} Sigma_{-i,-i}^{-1}, the Schur sd and the cdf limits of the
+  bounds recentred on the unconditional mean (App. A-5)."""
+  mean = np.atleast_1d(_f64(mean))
+  cov = np.atleast_2d(_f64(cov))
+  n = len(mean)
+  lims = np.stack([_f64(lo), _f64(hi)], -1) - np.expand_dims(mean, -1)
+  stdv = np.empty(n)
+  coef = np.zeros((n, max(n - 1, 0)))
+  for i in range(n):
+    ll = np.delete(cov[:, i].reshape([n, 1]), i, axis=0)
+    ru = np.delete(cov[i, :].reshape([1, n]), i, axis=1)
+    sub = np.delete(np.delete(cov, i, axis=1), i, axis=0)
+    row = ru.dot(np.linalg.inv(sub))
+    coef[i] = row.reshape(-1)
+    stdv[i] = np.sqrt(cov[i, i] - row.dot(ll).item())
+  cdfs = np.array([scipy.stats.norm.cdf(lim, loc=0., scale=stdv[i])
+                   for i, lim in enumerate(lims)])
+  return coef, stdv, cdfs
+
+
+def mvn_psd(mean, cov):
+  """scipy multivariate_normal's CovViaPSD: (whitening U, rank*log(2pi) +
+  log_pdet) exactly as scipy forms them (_multivariate.py _logpdf)."""
+  mvn = scipy.stats.multivariate_normal(_f64(mean), _f64(cov))
+  co = mvn.cov_object
+  const = co.rank * np.log(2 * np.pi) + co.log_pdet
+  return _f64(co._LP), float(const)
+
+
+class Engine:
+  """One libpbhip engine on one device, running one lowered model."""
+
+  def __init__(self, spec, device=0):
+    self.spec = normalize_spec(spec)
+    self.dim = self.spec['dim']
+    self._h = _c.c_void_p()
+    _lib.call('pbh_create', int(device), _c.byref(self._h))
+    self.device = device
+    self.n = 0
+    self._set_model()
+    if self.spec['proposal']['kind'] == 'gibbs':
+      self._set_gibbs()
+    else:
+      self._set_proposal()
+
+  # ---- model -------------------------------------------------------------
+  def _set_model(self):
+    s, d = self.spec, self.dim
+    tg = s['target']
+    m = _lib.PbhModel()
+    m.dim = d
+    m.target_kind = _lib.TARGET[tg['kind']]
+    m.pscale = _lib.PSCALE[s['pscale']]
+    m.scores = _lib.SCORES[s['scores']]
+    keep = []
+
+    def arr(a, conv=_f64):
+      a = conv(a)
+      keep.append(a)
+      return a
+
+    kind = tg['kind']
+    if kind == 'diag_gauss':
+      m.a, m.b = _dp(arr(tg['mu'])), _dp(arr(tg['sigma']))
+      m.c = _dp(arr(np.log(_f64(tg['sigma']))))
+    elif kind == 'norm_iid':
+      m.a = _dp(arr(tg['obs']))
+      m.n = len(tg['obs'])
+      m.i0, m.i1 = tg['loc'], tg['scale']
+    elif kind == 'gmm':
+      m.a, m.b = _dp(arr(tg['logw'])), _dp(arr(tg['mu']))
+      m.c, m.e = _dp(arr(tg['sd'])), _dp(arr(np.log(_f64(tg['sd']))))
+      m.n = len(tg['logw'])
+    elif kind in ('norm_pdf',):
+      m.a, m.b = _dp(arr(tg['loc'])), _dp(arr(tg['scale']))
+    elif kind == 'uniform_pdf':
+      m.a, m.b = _dp(arr(tg['lo'])), _dp(arr(tg['scale']))
+    elif kind == 'mvn':
+      U, const = mvn_psd(tg['mean'], tg['cov'])
+      m.a, m.b = _dp(arr(tg['mean'])), _dp(arr(U))
+      m.c = _dp(arr(np.array([const])))
+    pr = s['prior']
+    if pr is not None:
+      m.has_prior = 1
+      m.prior_lo, m.prior_hi = _dp(arr(pr['lo'])), _dp(arr(pr['hi']))
+      m.prior_lo_incl = _ip(arr(pr['lo_incl'], _i32))
+      m.prior_hi_incl = _ip(arr(pr['hi_incl'], _i32))
+      m.prior_logp = pr['logp']
+    m.ufun = _ip(arr(s['ufun'], _i32))
+    tr = s['tran']
+    m.tran_kind = _lib.TRAN[tr['kind']]
+    m.tran_sym = 1 if tr['sym'] else 0
+    if tr['kind'] == 'const':
+      m.tran_value = tr['value']
+    else:
+      m.tran_scale = tr['scale']
+      m.tran_offset = _dp(arr(tr['offset']))
+      m.tran_order = _ip(arr(tr['order'], _i32))
+    _lib.call('pbh_set_model', self._h, _c.byref(m))
+
+  def _set_proposal(self):
+    p, d = self.spec['proposal'], self.dim
+    q = _lib.PbhProposal()
+    q.kind = _lib.PROPOSAL[p['kind']]
+    keep = []
+
+    def arr(a, conv=_f64):
+      a = conv(a)
+      keep.append(a)
+      return a
+
+    if p['kind'] == 'gauss':
+      q.loc, q.scale = _dp(arr(p['loc'])), _dp(arr(p['scale']))
+      q.order = _ip(arr(p['order'], _i32))
+    elif p['kind'] == 'sphere':
+      q.delta = p['delta']
+      q.lengths = _dp(arr(p['lengths']))
+    elif p['kind'] == 'uniform':
+      q.delta_vec = _dp(arr(p['delta']))
+    _lib.call('pbh_set_proposal', self._h, _c.byref(q))
+
+  def _set_gibbs(self):
+    p = self.spec['proposal']
+    coef, stdv, cdfs = condcov_tables(p['mean'], p['cov'], p['lo'], p['hi'])
+    keep = [_f64(p['mean']), _f64(coef), _f64(stdv), _f64(cdfs)]
+    g = _lib.PbhGibbs()
+    g.mean, g.coef, g.stdv, g.cdf = [_dp(a) for a in keep]
+    g.tsteps = p['tsteps']
+    _lib.call('pbh_set_gibbs', self._h, _c.byref(g))
+
+  # ---- chains / randomness -------------------------------------------------
+  def init_chains(self, init, chain_offset=0):
+    """init [N, d] (or [d] broadcast to n chains via init_like)."""
+    init = _f64(init).reshape(-1, self.dim)
+    self.n = init.shape[0]
+    _lib.call('pbh_init_chains', self._h, _c.c_int64(self.n),
+              _c.c_int64(int(chain_offset)), _dp(init))
+    self.chain_offset = int(chain_offset)
+
+  def set_rng(self, mode='philox', seed=0):
+    _lib.call('pbh_set_rng', self._h, _lib.RNG[mode],
+              _c.c_uint64(int(seed) & (2 ** 64 - 1)))
+
+  def stream_width(self):
+    r = _c.c_int32()
+    _lib.call('pbh_stream_width', self._h, _c.byref(r))
+    return r.value
+
+  def upload_replay(self, streams):
+    """streams [T, R, N] in the reference's per-step consumption order."""
+    streams = _f64(streams)
+    T, R, N = streams.shape
+    if N != self.n or R != self.stream_width():
+      raise ValueError('replay stream shape {} does not match R={}, N={}'
+                       .format(streams.shape, self.stream_width(), self.n))
+    _lib.call('pbh_upload_replay', self._h, _c.c_int64(T), _dp(streams))
+
+  # ---- running -----------------------------------------------------------
+  def alloc_trace(self, capacity, thin=1, debug=False):
+    _lib.call('pbh_alloc_trace', self._h, _c.c_int64(int(capacity)),
+              int(thin), 1 if debug else 0)
+    self.debug = bool(debug)
+
+  def run(self, n_steps, steps_per_launch=0, sync=True):
+    _lib.call('pbh_run', self._h, _c.c_int64(int(n_steps)),
+              int(steps_per_launch))
+    if sync:
+      self.sync()
+
+  def sync(self):
+    _lib.call('pbh_sync', self._h)
+
+  def last_run_ms(self):
+    ms, nl = _c.c_double(), _c.c_int64()
+    _lib.call('pbh_last_run_ms', self._h, _c.byref(ms), _c.byref(nl))
+    return ms.value, nl.value
+
+  # ---- results -----------------------------------------------------------
+  def state(self):
+    x = np.empty((self.n, self.dim))
+    lp = np.empty(self.n)
+    _lib.call('pbh_get_state', self._h, _dp(x), _dp(lp))
+    return x, lp
+
+  def trace_len(self):
+    r = _c.c_int64()
+    _lib.call('pbh_trace_len', self._h, _c.byref(r))
+    return r.value
+
+  def trace(self, first=0, count=None, debug=None):
+    """Recorded steps as chain-major arrays shaped like the golden fixtures:
+    v_x [N, T, d], v_p [N, T], u [N, T] (uint8); with debug also p_x, p_p, s."""
+    count = self.trace_len() - first if count is None else count
+    n, d = self.n, self.dim
+    W = (n + 63) // 64
+    x = np.empty((count, d, n))
+    lp = np.empty((count, n))
+    acc = np.empty((count, W), np.uint64)
+    debug = self.debug if debug is None else debug
+    px = np.empty((count, d, n)) if debug else None
+    pp = np.empty((count, n)) if debug else None
+    sc = np.empty((count, n)) if debug else None
+    nul = _c.POINTER(_c.c_double)()
+    _lib.call('pbh_get_trace', self._h, _c.c_int64(first), _c.c_int64(count),
+              _dp(x), _dp(lp), acc.ctypes.data_as(_c.POINTER(_c.c_uint64)),
+              _dp(px) if debug else nul, _dp(pp) if debug else nul,
+              _dp(sc) if debug else nul)
+    bits = np.unpackbits(acc.view(np.uint8).reshape(count, W * 8),
+                         axis=1, bitorder='little')[:, :n]
+    out = {'v_x': x.transpose(2, 0, 1), 'v_p': lp.T,
+           'u': np.ascontiguousarray(bits.T)}
+    if debug:
+      out.update({'p_x': px.transpose(2, 0, 1), 'p_p': pp.T, 's': sc.T})
+    return out
+
+  def moments(self):
+    n, d = self.n, self.dim
+    s = np.empty((d, n))
+    q = np.empty((d, n))
+    na = np.empty(n, np.int64)
+    steps = _c.c_int64()
+    _lib.call('pbh_get_moments', self._h, _dp(s), _dp(q),
+              na.ctypes.data_as(_c.POINTER(_c.c_int64)), _c.byref(steps))
+    return {'sum': s.T.copy(), 'sumsq': q.T.copy(), 'n_acc': na,
+            'n_steps': steps.value}
+
+  def reset_moments(self):
+    _lib.call('pbh_reset_moments', self._h)
+
+  # ---- RCCL ---------------------------------------------------------------
+  @staticmethod
+  def rccl_unique_id():
+    buf = (_c.c_uint8 * 128)()
+    _lib.call('pbh_rccl_unique_id', buf)
+    return bytes(buf)
+
+  def rccl_init(self, rank, world, uid):
+    buf = (_c.c_uint8 * 128).from_buffer_copy(uid)
+    _lib.call('pbh_rccl_init', self._h, int(rank), int(world), buf)
+    self.world = int(world)
+
+  def rccl_allgather_moments(self):
+    d, n = self.dim, self.n
+    out = np.empty((self.world, 2 * d + 1, n))
+    _lib.call('pbh_rccl_allgather_moments', self._h, _dp(out))
+    return out
+
+  def rccl_allreduce_max(self, value):
+    v = _c.c_double(float(value))
+    _lib.call('pbh_rccl_allreduce_max', self._h, _c.byref(v))
+    return v.value
+
+  def close(self):
+    if getattr(self, '_h', None) is not None and self._h.value:
+      _lib.load().pbh_destroy(self._h)
+      self._h = _c.c_void_p()
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def __enter__(self):
+    return self
+
+  def __exit__(self, *exc):
+    self.close()

@@ -1,0 +1,180 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the oracle/reference.
+
+Replay mode feeds the kernels the reference's own legacy-MT19937 streams, so
+every golden workload must reproduce the reference traces step for step:
+  * accept decisions u: identical (0 flips);
+  * states and (log-)probabilities: relative error <= 1e-12 per step
+    (device exp/log/ndtri differ from glibc/NumPy SIMD by ulps; the
+    tolerance is SURVEY.md §7 step 4's);
+  * posterior moments over the traces: <= 1e-6 relative (north star).
+Philox mode (production RNG) is checked statistically and by invariants.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from oracle.workloads import golden_init
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def _engine(spec):
+  from probayes_amd import Engine
+  return Engine(spec)
+
+
+def _rel_err(a, b):
+  a, b = np.asarray(a, float), np.asarray(b, float)
+  both_nan = np.isnan(a) & np.isnan(b)
+  same = (a == b) | both_nan
+  den = np.maximum(np.abs(b), np.finfo(float).tiny)
+  err = np.where(same, 0., np.abs(a - b) / den)
+  return float(err.max()) if err.size else 0.
+
+
+def _run_replay(spec, init, streams, debug=True):
+  T = streams.shape[0]
+  eng = _engine(spec)
+  eng.init_chains(init)
+  eng.set_rng('replay')
+  eng.upload_replay(streams)
+  eng.alloc_trace(T, 1, debug=debug)
+  eng.run(T)
+  out = eng.trace()
+  mom = eng.moments()
+  eng.close()
+  return out, mom
+
+
+@pytest.mark.parametrize('name', sorted(oracle.WORKLOADS))
+def test_replay_matches_reference_golden(name):
+  g = oracle.load_golden(name)
+  spec = oracle.golden_spec(name, g)
+  n, t = g['v_x'].shape[:2]
+  streams = oracle.legacy_streams(spec, g['seeds'], t)
+  out, mom = _run_replay(spec, golden_init(name, n), streams)
+  flips = int(np.sum(out['u'] != g['u']))
+  assert flips == 0, '{}: {} accept flips'.format(name, flips)
+  assert _rel_err(out['v_x'], g['v_x']) <= RTOL
+  assert _rel_err(out['v_p'], g['v_p']) <= RTOL
+  assert _rel_err(out['p_x'], g['p_x']) <= RTOL
+  assert _rel_err(out['p_p'], g['p_p']) <= RTOL
+  if spec['scores'] != 'gibbs':
+    assert _rel_err(out['s'], g['s']) <= 1e-10
+  # in-kernel moments == moments of the recorded trace
+  np.testing.assert_allclose(mom['sum'], g['v_x'].sum(axis=1), rtol=1e-9,
+                             atol=1e-9)
+  assert np.array_equal(mom['n_acc'], g['u'].sum(axis=1))
+
+
+@pytest.mark.parametrize('name,n,t', [('diag10', 1024, 400),
+                                      ('metrohast_norm1d', 256, 400),
+                                      ('gibbs8', 512, 256),
+                                      ('gmm2', 1024, 400)])
+def test_replay_posterior_moments_vs_oracle(name, n, t):
+  """Posterior moments of GPU replay runs vs the oracle: 1e-6 relative."""
+  spec = oracle.golden_spec(name)
+  seeds = np.arange(50000, 50000 + n)
+  streams = oracle.legacy_streams(spec, seeds, t)
+  init = golden_init(name, n)
+  run = oracle.run_gibbs if spec['scores'] == 'gibbs' else oracle.run_mh
+  ref = run(spec, init, streams)
+  out, _ = _run_replay(spec, init, streams, debug=False)
+  flips = np.sum(out['u'] != ref['u'])
+  assert flips <= max(1, n * t // 10 ** 6), flips
+  for k in ('v_x',):
+    m_ref, m_gpu = ref[k].mean(axis=1), out[k].mean(axis=1)
+    sd = ref[k].std(axis=1)
+    den = np.maximum(np.abs(m_ref), sd)
+    assert np.max(np.abs(m_gpu - m_ref) / den) <= 1e-6
+    v_ref, v_gpu = ref[k].var(axis=1), out[k].var(axis=1)
+    assert np.max(np.abs(v_gpu - v_ref) / np.maximum(v_ref, 1e-300)) <= 1e-6
+
+
+def _diag10_spec():
+  return oracle.golden_spec('diag10')
+
+
+def test_philox_diag10_statistics_and_invariants():
+  """cfg2 model in production (Philox) mode: the posterior matches the
+  target within Monte-Carlo error; traces are deterministic and invariant to
+  how chains are sharded (global chain ids key the RNG)."""
+  spec = _diag10_spec()
+  n, t, burn = 8192, 1200, 200
+  eng = _engine(spec)
+  eng.init_chains(np.zeros((n, 10)))
+  eng.set_rng('philox', seed=1234)
+  eng.run(burn)
+  eng.reset_moments()
+  eng.run(t - burn)
+  mom = eng.moments()
+  x_end, _ = eng.state()
+  eng.close()
+  steps = mom['n_steps']
+  mean = mom['sum'].sum(0) / (n * steps)
+  var = mom['sumsq'].sum(0) / (n * steps) - mean ** 2
+  mu, sg = spec['target']['mu'], spec['target']['sigma']
+  # generous MC bound: autocorrelated chains, n*steps ~ 8e6 draws
+  assert np.all(np.abs(mean - mu) < 0.05 * sg), (mean, mu)
+  assert np.all(np.abs(var / sg ** 2 - 1) < 0.05), var / sg ** 2
+  acc = mom['n_acc'].sum() / (n * steps)
+  assert 0.05 < acc < 0.6
+
+  # determinism + sharding invariance on a short run with a trace
+  def run(n0, n1):
+    e = _engine(spec)
+    e.init_chains(np.zeros((n1 - n0, 10)), chain_offset=n0)
+    e.set_rng('philox', seed=99)
+    e.alloc_trace(50, 1)
+    e.run(50, steps_per_launch=17)
+    tr = e.trace()
+    e.close()
+    return tr
+  full = run(0, 4096)
+  again = run(0, 4096)
+  lo, hi = run(0, 2048), run(2048, 4096)
+  np.testing.assert_array_equal(full['v_x'], again['v_x'])
+  np.testing.assert_array_equal(full['v_x'][:2048], lo['v_x'])
+  np.testing.assert_array_equal(full['v_x'][2048:], hi['v_x'])
+  np.testing.assert_array_equal(full['u'][2048:], hi['u'])
+
+
+def test_thinning_and_launch_split_equivalence():
+  spec = oracle.golden_spec('gmm2')
+  n, t = 300, 60          # ragged: n not a multiple of 64
+  seeds = np.arange(7, 7 + n)
+  streams = oracle.legacy_streams(spec, seeds, t)
+  init = golden_init('gmm2', n)
+  ref = oracle.run_mh(spec, init, streams)
+  eng = _engine(spec)
+  eng.init_chains(init)
+  eng.set_rng('replay')
+  eng.upload_replay(streams)
+  eng.alloc_trace(t // 3, 3)
+  eng.run(t, steps_per_launch=7)
+  tr = eng.trace()
+  eng.close()
+  assert tr['v_x'].shape == (n, t // 3, 2)
+  assert _rel_err(tr['v_x'], ref['v_x'][:, 2::3]) <= RTOL
+  assert np.array_equal(tr['u'], ref['u'][:, 2::3])
+
+
+def test_engine_errors_are_loud():
+  from probayes_amd._lib import PbhError
+  spec = _diag10_spec()
+  eng = _engine(spec)
+  with pytest.raises(PbhError):
+    eng.run(5)                      # no chains yet
+  eng.init_chains(np.zeros((64, 10)))
+  eng.set_rng('replay')
+  with pytest.raises(PbhError):
+    eng.run(5)                      # replay without a stream
+  eng.set_rng('philox', 1)
+  eng.alloc_trace(4, 1)
+  with pytest.raises(PbhError):
+    eng.run(5)                      # trace capacity exceeded
+  eng.run(4)
+  assert eng.trace_len() == 4
+  eng.close()
