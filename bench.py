@@ -85,6 +85,7 @@ def main():
   ap.add_argument('--chains', type=int, default=65536, help='per GPU')
   ap.add_argument('--steps-per-launch', type=int, default=250)
   ap.add_argument('--no-trace', action='store_true')
+  ap.add_argument('--rng', default='philox', choices=['philox', 'philox_f64'])
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--traffic-bytes', type=float, default=None,
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
@@ -101,7 +102,7 @@ def main():
   n = args.chains
   eng = Engine(spec, device=local)
   eng.init_chains(np.zeros((n, D)), chain_offset=rank * n)
-  eng.set_rng('philox', seed=20261015)
+  eng.set_rng(args.rng, seed=20261015)
   if not args.no_trace:
     eng.alloc_trace(args.warmup + args.steps, 1)
 
@@ -152,7 +153,10 @@ def main():
         'config': {'workload': 'cfg2: 10-dim diagonal-Gaussian random-walk '
                                'MH, {} chains/GPU, full trace every step'
                                .format(n),
-                   'chains_per_gpu': n, 'dim': D, 'rng': 'philox4x32-10',
+                   'chains_per_gpu': n, 'dim': D,
+                   'rng': 'philox4x32-10 ({})'.format(
+                       'fp32 Box-Muller normals, exact sign symmetry'
+                       if args.rng == 'philox' else 'fp64 Box-Muller normals'),
                    'trace': not args.no_trace, 'steps_per_launch': spl,
                    'parallelism': 'chain-sharded x{}'.format(world)},
         'roofline': {'bound': 'hbm', 'achieved': achieved,

@@ -58,8 +58,13 @@ enum pbh_proposal_kind {
   PBH_PROP_GIBBS = 4    /* CondCov conditional draw, cond_cov.py:42-65        */
 };
 enum pbh_rng_mode {
-  PBH_RNG_REPLAY = 0, /* randoms read from a caller-supplied [T][R][N] stream  */
-  PBH_RNG_PHILOX = 1  /* Philox-4x32-10 keyed by (seed, global chain id)      */
+  PBH_RNG_REPLAY = 0,    /* randoms read from a caller-supplied [T][R][N]
+                            stream; reference arithmetic (parity mode)        */
+  PBH_RNG_PHILOX = 1,    /* production: Philox-4x32-10 keyed by (seed, global
+                            chain id); fp32 Box-Muller normals with exact sign
+                            symmetry, FMA-corrected divisions                 */
+  PBH_RNG_PHILOX_F64 = 2 /* Philox-4x32-10 with fp64 Box-Muller normals and
+                            the reference arithmetic of REPLAY                 */
 };
 
 /* Joint density + acceptance (replaces RF.set_prob/set_tran + SP.set_scores:
@@ -71,13 +76,14 @@ typedef struct pbh_model {
   int32_t pscale;       /* enum pbh_pscale of the density (pscales.py:21-41)   */
   int32_t scores;       /* enum pbh_scores (sp_utils.py:87-91)                */
   /* target parameters (meaning per kind):
-   *   DIAG_GAUSS : a = mu[d], b = sigma[d], c = log(sigma)[d]
+   *   DIAG_GAUSS : a = mu[d], b = sigma[d], c = log(sigma)[d], e = 1/sigma[d]
    *   NORM_IID   : a = obs[n], n = n_obs, i0 = loc dim, i1 = scale dim
    *   GMM        : a = logw[K], b = mu[K*d], c = sd[K], e = log(sd)[K], n = K
    *   NORM_PDF   : a = loc[d], b = scale[d]
    *   UNIFORM_PDF: a = lo[d], b = scale[d]
-   *   MVN        : a = mean[d] (in permuted order), b = prec_U[d*d] row-major,
-   *                c = {rank*log(2pi) + log_pdet}, perm = permutation[d]      */
+   *   MVN        : a = mean[d], b = whitening U[d*d] row-major (scipy
+   *                CovViaPSD._LP), c = {rank*log(2pi) + log_pdet}; the density
+   *                is taken at x[perm] with prob.py:354-357's fixed perm     */
   const double *a, *b, *c, *e;
   const int32_t *perm;
   int64_t n;

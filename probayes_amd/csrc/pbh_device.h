@@ -61,6 +61,36 @@ __device__ __forceinline__ void box_muller(u32x4 w, double &z0, double &z1) {
   z1 = r * s;
 }
 
+// Production normals (PBH_RNG_PHILOX): two standard-normal pairs per Philox
+// block from the hardware fp32 transcendentals (v_log_f32, v_sin_f32,
+// v_cos_f32), widened to fp64.  The magnitude r = sqrt(-2 ln u1) uses 24-bit
+// u1 in (0, 1] (|z| <= 5.77) and the angle lives in one quadrant; each
+// coordinate's sign is an independent Philox bit, so the proposal density is
+// EXACTLY symmetric, f(delta) = f(-delta) -- the only property the random-walk
+// MH acceptance relies on (sp_utils.py:56 drops q).  Its precision (~2^-22
+// relative) affects only proposal shape, never the fp64 chain arithmetic.
+__device__ __forceinline__ double fast_normal_pair(uint32_t wu, uint32_t wa,
+                                                   double &z1) {
+  const float u1 = (float)((wu >> 8) + 1u) * 5.9604644775390625e-08f;  // 2^-24
+  const float rev = (float)(wa >> 8) * 1.4901161193847656e-08f;      // [0, 1/4)
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f *    // -2 ln 2
+                                         __builtin_amdgcn_logf(u1)); // log2
+  const float c = r * __builtin_amdgcn_cosf(rev);   // cos(2 pi rev)
+  const float s = r * __builtin_amdgcn_sinf(rev);
+  const uint64_t s0 = (uint64_t)(wa & 1u) << 63, s1 = (uint64_t)(wa & 2u) << 62;
+  z1 = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, (double)s) ^ s1);
+  return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, (double)c) ^ s0);
+}
+
+// a / b for a loop-invariant b with its reciprocal rb = 1/b: one FMA
+// correction of a*rb (Markstein) -- the correctly rounded quotient in all but
+// rare ties; used only on the production path (parity paths divide).
+__device__ __forceinline__ double div_by(double a, double b, double rb) {
+  const double q = a * rb;
+  const double e = __builtin_fma(-q, b, a);
+  return __builtin_fma(e, rb, q);
+}
+
 // ---------------------------------------------------------------------------
 // NumPy pairwise summation (numpy/_core/src/umath/loops_utils.h.src
 // pairwise_sum, numpy 2.2): < 8 terms sequential from 0, <= 128 terms with

@@ -215,7 +215,7 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
   const double *A = m->a, *B = m->b, *C = m->c, *E = m->e;
   int64_t na = 0, nb = 0, nc = 0, ne = 0;
   switch (m->target_kind) {
-    case PBH_TARGET_DIAG_GAUSS: na = nb = nc = d; break;
+    case PBH_TARGET_DIAG_GAUSS: na = nb = nc = ne = d; break;
     case PBH_TARGET_NORM_IID:
       if (m->n < 1) return fail(PBH_ERR_ARG, "NORM_IID needs n_obs >= 1");
       if (m->i0 < 0 || m->i0 >= d || m->i1 < 0 || m->i1 >= d)
@@ -416,7 +416,8 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
 
 int pbh_set_rng(pbh_engine *e, int32_t mode, uint64_t seed) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
-  if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX)
+  if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX &&
+      mode != PBH_RNG_PHILOX_F64)
     return fail(PBH_ERR_ARG, "bad rng mode %d", mode);
   e->rng = mode;
   e->seed = seed;

@@ -84,18 +84,27 @@ __device__ __forceinline__ double mvn_density(const KArgs &a,
   return a.pscale == PBH_PSCALE_LIN ? exp(logpdf) : logpdf;
 }
 
-template <int D>
+template <int D, int TGT, bool FAST>
 __device__ __forceinline__ double joint_density(const KArgs &a,
                                                 const double (&x)[D],
                                                 const double *obs_lds,
                                                 bool use_lds) {
   double out = 0.0;
-  switch (a.target) {
+  switch (TGT ? TGT : a.target) {
     case PBH_TARGET_DIAG_GAUSS: {
       // lp(**kw) = sum(norm.logpdf(kw[k], mu_k, sigma_k)): Python sum from 0
+      if (FAST) {
+        // production path: FMA-corrected division by the constant sigma
 #pragma unroll
-      for (int k = 0; k < D; ++k)
-        out = out + norm_logpdf(x[k], a.ta[k], a.tb[k], a.tc[k], a.norm_logC);
+        for (int k = 0; k < D; ++k) {
+          const double y = div_by(x[k] - a.ta[k], a.tb[k], a.te[k]);
+          out = out + (((y * y) * -0.5 - a.norm_logC) - a.tc[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          out = out + norm_logpdf(x[k], a.ta[k], a.tb[k], a.tc[k], a.norm_logC);
+      }
       break;
     }
     case PBH_TARGET_NORM_IID: {
@@ -186,12 +195,16 @@ __device__ __forceinline__ double div_prob(const KArgs &a, double num,
 
 // hastings_scores / metropolis_scores (sp_utils.py:19-64).  Returns false
 // when the score is None (auto-accept), else writes s.
+// eB = rescale(lp) of the current state (cached across steps, updated on
+// accept by the caller with eA = rescale(lpp)); the division is the same
+// IEEE operation as div_prob's, so caching changes no bits.
 template <int D>
 __device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
                                       const double (&xp)[D], double lp,
-                                      double lpp, double &s) {
+                                      double lpp, double eA, double eB,
+                                      double &s) {
   if (a.scores == PBH_SCORES_METROPOLIS) {
-    const double q = div_prob(a, lpp, lp);
+    const double q = eA / np_max_tiny(eB);
     s = q < 1. ? q : 1.;  // Python min(1., q)
     return true;
   }
@@ -218,7 +231,7 @@ __device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
   if (qt <= 0.) return false;                      // sp_utils.py:53-54
   double r;
   if (a.tran_sym) {
-    r = div_prob(a, lpp, lp);                      // :56
+    r = eA / np_max_tiny(eB);                      // :56
   } else {
     // reval_tran returns the forward value (rf.py:536): r~ == q~
     r = div_prob(a, lpp * qt, lp * qt);            // :62-64
@@ -230,8 +243,15 @@ __device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
 // ---------------------------------------------------------------------------
 // MH kernel: n_steps fused chain-steps, one chain per lane
 // ---------------------------------------------------------------------------
-template <int D, int RNG>
+template <int D, int RNG, int TGT, int PROP>
 __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
+  // TGT / PROP != 0 compile the kernel for one target / proposal form;
+  // 0 keeps the wave-uniform runtime switch (any model, one binary).
+  // FAST = production Philox path (fp32 normals, FMA-corrected divisions);
+  // REPLAY and PHILOX_F64 keep the reference's arithmetic exactly.
+  constexpr bool FAST = RNG == PBH_RNG_PHILOX;
+  const int prop = PROP ? PROP : a.prop;
+  const bool lin = a.pscale == PBH_PSCALE_LIN;
   extern __shared__ double s_obs[];
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = c < a.n;
@@ -239,7 +259,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   const int lane = threadIdx.x & 63;
 
   bool use_lds = false;
-  if (a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
+  if ((TGT == 0 || TGT == PBH_TARGET_NORM_IID) &&
+      a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
     for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = a.ta[j];
     __syncthreads();
     use_lds = true;
@@ -253,6 +274,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     mq[k] = 0.;
   }
   double lp = a.lp[cc];
+  double eB = lin ? lp : exp_logp(lp, a.log_npi);
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
 
@@ -266,8 +288,32 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 #pragma unroll
       for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
       thr = row[(int64_t)D * a.n];
+    } else if (FAST && prop == PBH_PROP_GAUSS) {
+      // two normal pairs per Philox block; an odd pair count leaves the
+      // block's second half for the 53-bit threshold
+      constexpr int P = (D + 1) / 2;
+#pragma unroll
+      for (int q = 0; q < (P + 1) / 2; ++q) {
+        const u32x4 w = philox4x32_10(ctr(q, g, chain), a.seed_lo, a.seed_hi);
+        double z1;
+        const double z0 = fast_normal_pair(w.x, w.z, z1);
+        if (4 * q < D) r[4 * q] = z0;
+        if (4 * q + 1 < D) r[4 * q + 1] = z1;
+        if (2 * q + 1 < P) {
+          double z3;
+          const double z2 = fast_normal_pair(w.y, w.w, z3);
+          if (4 * q + 2 < D) r[4 * q + 2] = z2;
+          if (4 * q + 3 < D) r[4 * q + 3] = z3;
+        } else {
+          thr = u01(w.y, w.w);
+        }
+      }
+      if (P % 2 == 0) {
+        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+        thr = u01(w.x, w.y);
+      }
     } else {
-      if (a.prop == PBH_PROP_GAUSS) {
+      if (prop == PBH_PROP_GAUSS) {
 #pragma unroll
         for (int p = 0; p < (D + 1) / 2; ++p) {
           double z0, z1;
@@ -290,11 +336,11 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     double xp[D];
     {
       double dl[D];
-      if (a.prop == PBH_PROP_GAUSS) {
+      if (prop == PBH_PROP_GAUSS) {
         // scipy rv_generic.rvs: z * scale + loc
 #pragma unroll
         for (int k = 0; k < D; ++k) dl[k] = r[k] * a.pscl[k] + a.ploc[k];
-      } else if (a.prop == PBH_PROP_UNIFORM) {
+      } else if (prop == PBH_PROP_UNIFORM) {
         // np.random.uniform(-delta, delta) = low + (high - low) * u
 #pragma unroll
         for (int k = 0; k < D; ++k) {
@@ -320,18 +366,20 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         xp[k] = ((a.ufun >> k) & 1u) ? exp(log(x[k]) + dl[k]) : x[k] + dl[k];
     }
     // ---- density, score, accept ----
-    const double lpp = joint_density<D>(a, xp, s_obs, use_lds);
+    const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
+    const double eA = lin ? lpp : exp_logp(lpp, a.log_npi);
     double sc = __builtin_nan("");
     bool acc;
     if (!a.has_pred && s == 0) {
       acc = true;                                  // s = None on step 1
     } else {
-      acc = !score<D>(a, x, xp, lp, lpp, sc) || (sc >= thr);
+      acc = !score<D>(a, x, xp, lp, lpp, eA, eB, sc) || (sc >= thr);
     }
     if (acc) {
 #pragma unroll
       for (int k = 0; k < D; ++k) x[k] = xp[k];
       lp = lpp;
+      eB = eA;
     }
     nacc += acc ? 1 : 0;
 #pragma unroll
@@ -467,13 +515,39 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
 
 }  // namespace
 
-template <int D>
-hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
+template <int D, int TGT, int PROP>
+void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
   const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
   if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_REPLAY>), grid, block, lds, st, a);
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_REPLAY, TGT, PROP>), grid, block,
+                       lds, st, a);
+  else if (a.rng == PBH_RNG_PHILOX)
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX, TGT, PROP>), grid, block,
+                       lds, st, a);
   else
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX>), grid, block, lds, st, a);
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX_F64, TGT, PROP>), grid,
+                       block, lds, st, a);
+}
+
+template <int D>
+hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
+  // Specialised forms: the cfg2 diagonal Gaussian with the callable Gaussian
+  // delta at every d; the other example forms at the small d they use.
+  if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS) {
+    launch_mh_spec<D, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>(a, st, lds);
+    return hipGetLastError();
+  }
+  if constexpr (D <= 4) {
+    if (a.target == PBH_TARGET_GMM && a.prop == PBH_PROP_GAUSS) {
+      launch_mh_spec<D, PBH_TARGET_GMM, PBH_PROP_GAUSS>(a, st, lds);
+      return hipGetLastError();
+    }
+    if (a.target == PBH_TARGET_NORM_IID && a.prop == PBH_PROP_SPHERE) {
+      launch_mh_spec<D, PBH_TARGET_NORM_IID, PBH_PROP_SPHERE>(a, st, lds);
+      return hipGetLastError();
+    }
+  }
+  launch_mh_spec<D, 0, 0>(a, st, lds);
   return hipGetLastError();
 }
 

@@ -103,6 +103,7 @@ class Engine:
     if kind == 'diag_gauss':
       m.a, m.b = _dp(arr(tg['mu'])), _dp(arr(tg['sigma']))
       m.c = _dp(arr(np.log(_f64(tg['sigma']))))
+      m.e = _dp(arr(1.0 / _f64(tg['sigma'])))
     elif kind == 'norm_iid':
       m.a = _dp(arr(tg['obs']))
       m.n = len(tg['obs'])
