@@ -77,6 +77,21 @@ def cpu_baseline(budget_s=12.0):
                     'core, BASELINE.md)'.format(n, t, reps)}
 
 
+def measured_traffic(chains, spl, rng, trace):
+  """HBM bytes per launch of this exact launch shape, from the newest
+  profiles/r*_traffic.json (rocprofv3 PMC passes of scripts/profile.sh), or
+  None when no profile matches."""
+  import glob
+  files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic.json')))
+  if not files or not trace or rng != 'philox':
+    return None
+  with open(files[-1]) as f:
+    t = json.load(f)
+  if t.get('chains') != chains or t.get('steps_per_launch') != spl:
+    return None
+  return t['bytes_per_launch']
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -162,7 +177,9 @@ def main():
         'roofline': {'bound': 'hbm', 'achieved': achieved,
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS,
-                     'traffic': args.traffic_bytes,
+                     'traffic': args.traffic_bytes if args.traffic_bytes
+                                else measured_traffic(n, spl, args.rng,
+                                                      not args.no_trace),
                      'bytes_per_chain_step': bpcs,
                      'kernel': 'mh_kernel<10, PHILOX>',
                      'avg_launch_ms': avg_launch_s * 1e3,
