@@ -96,7 +96,9 @@ def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=1000)
-  ap.add_argument('--warmup', type=int, default=100)
+  ap.add_argument('--warmup', type=int, default=250,
+                  help='untimed steps; a multiple of --steps-per-launch keeps '
+                  'every dispatch the same shape as the timed ones')
   ap.add_argument('--chains', type=int, default=65536, help='per GPU')
   ap.add_argument('--steps-per-launch', type=int, default=250)
   ap.add_argument('--no-trace', action='store_true')
