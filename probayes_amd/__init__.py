@@ -9,3 +9,8 @@ __version__ = '0.1.0'
 
 from probayes_amd.spec import make_spec, normalize_spec  # noqa: F401
 from probayes_amd.engine import Engine  # noqa: F401
+from probayes_amd.rv import RV, RF  # noqa: F401,E402
+from probayes_amd.sp import SP  # noqa: F401,E402
+from probayes_amd.pd import PD  # noqa: F401,E402
+from probayes_amd.lower import NotLowerable  # noqa: F401,E402
+from probayes_amd import models  # noqa: F401,E402

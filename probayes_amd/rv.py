@@ -1,0 +1,140 @@
+"""RV and RF: the variable / field layer of the SP facade.
+
+RV mirrors probayes rv.py / variable.py for what the MH path reads from it:
+the value set and its bound inclusivity (variable.py:352-366: a limit wrapped
+in a tuple is exclusive), the (log, exp) change of variable set_ufun
+(variable.py:641-697), the transformed length (variable.py:313-342) and the
+default uniform prior -log(length) (rv.py:153-166).  RF mirrors rf.py's
+set_prob / set_tran / set_delta / set_tfun holders.  `x & y` builds an RF
+(ops.py:4-75).
+"""
+import collections
+
+import numpy as np
+
+
+class RV:
+  """A random variable (rv.py:28)."""
+
+  def __init__(self, name, vtype=float, vset=None, pscale=None, *args, **kwds):
+    if vtype not in (float, np.float64, 'float'):
+      raise NotImplementedError(
+          'RV {}: only float variables are on the GPU MH path'.format(name))
+    self.name = str(name)
+    self.vtype = float
+    self.vset = vset
+    self.pscale = pscale
+    self.ufun = None
+    self._log_ufun = False
+    self._parse_vset(vset)
+
+  def _parse_vset(self, vset):
+    if vset is None:
+      vset = (-np.inf, np.inf)
+    vset = list(vset)
+    if len(vset) != 2:
+      raise ValueError('float RV vset needs two limits, got {}'.format(vset))
+    lims, incl = [], []
+    for v in vset:
+      if isinstance(v, tuple):
+        lims.append(float(v[0]))
+        incl.append(False)
+      else:
+        lims.append(float(v))
+        incl.append(True)
+    self.vlims = np.array([min(lims), max(lims)])
+    self.lo_incl, self.hi_incl = incl[0], incl[1]
+
+  def set_ufun(self, ufun=None, *args, **kwds):
+    """Change of variable (variable.py:641-697).  Only (np.log, np.exp) is
+    lowered to the kernels."""
+    self.ufun = ufun
+    if ufun is None:
+      self._log_ufun = False
+      return
+    fwd, inv = ufun
+    if fwd is not np.log or inv is not np.exp:
+      raise NotImplementedError(
+          'RV {}: only the (np.log, np.exp) ufun is lowered'.format(self.name))
+    self._log_ufun = True
+
+  @property
+  def log_ufun(self):
+    return self._log_ufun
+
+  @property
+  def ulims(self):
+    """Transformed limits (variable.py:332-335)."""
+    return np.log(self.vlims) if self._log_ufun else self.vlims
+
+  @property
+  def length(self):
+    """max(ulims) - min(ulims) (variable.py:336)."""
+    ul = self.ulims
+    return max(ul) - min(ul)
+
+  @property
+  def lhv(self):
+    L = self.length
+    return np.log(L) if np.isfinite(L) else np.inf
+
+  def __and__(self, other):
+    return RF(self, other)
+
+  def __repr__(self):
+    return self.name
+
+
+class RF:
+  """A random field of RVs (rf.py:25) holding prob / tran / delta specs."""
+
+  def __init__(self, *args):
+    rvs = []
+    for a in args:
+      if isinstance(a, RV):
+        rvs.append(a)
+      elif isinstance(a, RF):
+        rvs.extend(a.rvs)
+      else:
+        raise TypeError('RF takes RVs or RFs, not {}'.format(type(a)))
+    names = [v.name for v in rvs]
+    if len(set(names)) != len(names):
+      raise ValueError('repeated variable names {}'.format(names))
+    self.rvs = rvs
+    self.prob = None
+    self.tran = None
+    self.tran_kwds = {}
+    self.delta = None
+    self.delta_args = ()
+    self.delta_kwds = {}
+    self.tfun = None
+    self.Delta = collections.namedtuple('Delta', names)
+
+  @property
+  def keylist(self):
+    return [v.name for v in self.rvs]
+
+  def __and__(self, other):
+    return RF(self, other)
+
+  def set_prob(self, prob=None, *args, **kwds):
+    self.prob = (prob, args, kwds)
+
+  def set_tran(self, tran=None, *args, **kwds):
+    """rf.py:169-239: a callable, a (forward, reverse) tuple, a scipy
+    multivariate_normal (CondCov Gibbs, tsteps=) or an RF to delegate to."""
+    kwds = dict(kwds)
+    self.tran = (tran, args, kwds)
+
+  def set_delta(self, delta=None, *args, **kwds):
+    """field.py:220-317: scalar in a tuple (spherical), in a list (uniform
+    per variable), or a callable returning Delta(...)."""
+    self.delta = delta
+    self.delta_args = args
+    self.delta_kwds = dict(kwds)
+
+  def set_tfun(self, tfun=None, *args, **kwds):
+    self.tfun = (tfun, args, kwds)
+
+  def __repr__(self):
+    return '&'.join(self.keylist)

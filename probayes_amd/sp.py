@@ -1,0 +1,446 @@
+"""SP: the stochastic-process facade (mirrors probayes sp.py / sd.py).
+
+The calls examples/mcmc makes -- SP(...), set_prob, set_tran, set_delta,
+set_scores, set_thresh, set_update, Delta, sampler, walk, SP(samples) and the
+summary fields v[key], v.prob, v.rescaled(), u.count(True) -- keep their
+reference meaning.  Underneath, a sampler lowers the model to a kernel spec
+(probayes_amd.lower) and runs every step of every chain in the HIP engine;
+the reference's per-step Python call stack never runs.
+
+Extensions over the reference (keyword-only, defaults keep its behaviour):
+  chains=N   run N independent chains in one batch (values become [T, N]);
+  rng=       'legacy' (default for one chain: NumPy's GLOBAL legacy stream,
+             exactly as the reference draws it, so seeded scripts reproduce
+             the reference's chains), 'legacy' with seeds=[...] (chain c uses
+             RandomState(seeds[c])), 'philox' (production, seed=) or
+             'philox_f64';
+  device=, thin=, steps_per_launch=.
+"""
+import collections
+
+import numpy as np
+import scipy.stats
+
+from probayes_amd import lower as L
+from probayes_amd import replay
+from probayes_amd.engine import Engine
+from probayes_amd.pd import PD
+from probayes_amd.pscales import is_log
+from probayes_amd.rv import RF, RV
+
+MCMC_SAMPLERS = ('metropolis', 'hastings', 'gibbs')   # sp_utils.py:87-91
+
+
+class FlagArray(np.ndarray):
+  """Update flags u with the list API the examples use (u.count(True))."""
+
+  def count(self, value=True):
+    return int(np.sum(self == bool(value)))
+
+
+def _as_rf(a):
+  if isinstance(a, RF):
+    return a
+  if isinstance(a, RV):
+    return RF(a)
+  raise TypeError('SP takes RVs or RFs, not {}'.format(type(a)))
+
+
+def _key(k):
+  return k.name if isinstance(k, RV) else str(k)
+
+
+class SP:
+  """A stochastic process over the roots' variables (sp.py:14)."""
+
+  def __init__(self, *args):
+    rfs = [_as_rf(a) for a in args]
+    if len(rfs) == 1:
+      self.leafs, self.roots = None, rfs[0]
+    elif len(rfs) == 2:
+      self.leafs, self.roots = rfs
+    else:
+      raise NotImplementedError('SP takes one RF or (stats, paras)')
+    self.Delta = self.roots.Delta
+    self._prob = None
+    self._tran = None      # (tran, args, kwds) or an RF to delegate to
+    self._delta = None     # (delta, args, kwds) or an RF
+    self._tfun = None
+    self._scores = self._thresh = self._update = None
+
+  # ---- specification (sp.py:57-100, rf.py:91-304, field.py:220-317) -----
+  @property
+  def keylist(self):
+    return self.roots.keylist
+
+  def set_prob(self, prob=None, *args, **kwds):
+    self._prob = (prob, args, dict(kwds))
+
+  def set_tran(self, tran=None, *args, **kwds):
+    self._tran = tran if isinstance(tran, RF) else (tran, args, dict(kwds))
+
+  def set_delta(self, delta=None, *args, **kwds):
+    self._delta = delta if isinstance(delta, RF) else (delta, args, dict(kwds))
+
+  def set_tfun(self, tfun=None, *args, **kwds):
+    self._tfun = tfun
+
+  def set_scores(self, scores=None, *args, **kwds):
+    self._scores = scores
+    if scores in MCMC_SAMPLERS:
+      self._thresh = self._thresh or scores
+      self._update = self._update or scores
+    elif scores is not None:
+      raise L.NotLowerable('custom scores callables have no kernel')
+
+  def set_thresh(self, thresh=None, *args, **kwds):
+    if thresh is not None and thresh not in MCMC_SAMPLERS:
+      raise L.NotLowerable('custom thresh callables have no kernel')
+    self._thresh = thresh
+
+  def set_update(self, update=None, *args, **kwds):
+    if update is not None and update not in MCMC_SAMPLERS:
+      raise L.NotLowerable('custom update callables have no kernel')
+    self._update = update
+
+  # ---- lowering -----------------------------------------------------------
+  def _pscale(self, kw_pscale):
+    if kw_pscale is not None:
+      return 'log' if is_log(kw_pscale) else 'lin'
+    rvs = list(self.roots.rvs) + (list(self.leafs.rvs) if self.leafs else [])
+    return 'log' if any(is_log(v.pscale) for v in rvs) else 'lin'
+
+  def _lower_target(self, extra, iid):
+    if self._prob is None:
+      raise L.NotLowerable('set_prob() first')
+    prob, args, kwds = self._prob
+    kwds = dict(kwds)
+    pscale_kw = kwds.pop('pscale', None)
+    order = kwds.pop('order', None)
+    names = self.keylist
+    if hasattr(prob, 'pbh_target'):
+      return dict(prob.pbh_target), pscale_kw or prob.pbh_pscale
+    if prob is scipy.stats.multivariate_normal:
+      if len(args) < 2:
+        raise L.NotLowerable('multivariate_normal needs (mean, cov)')
+      return {'kind': 'mvn', 'mean': np.asarray(args[0], np.float64),
+              'cov': np.asarray(args[1], np.float64)}, self._pscale(pscale_kw)
+    is_logpdf = L.is_same_callable(prob, scipy.stats.norm.logpdf)
+    is_pdf = L.is_same_callable(prob, scipy.stats.norm.pdf)
+    is_updf = L.is_same_callable(prob, scipy.stats.uniform.pdf)
+    if is_logpdf or is_pdf or is_updf:
+      order = order or {names[0]: 0}
+      slot = {}
+      for k, v in order.items():
+        slot[v] = _key(k)
+      loc = kwds.get('loc', args[0] if len(args) > 0 else 0.)
+      scale = kwds.get('scale', args[1] if len(args) > 1 else 1.)
+      xname = slot.get(0)
+      if 'loc' in slot or 'scale' in slot:
+        # data variable at position 0, roots as loc / scale (iid product)
+        if not (is_logpdf and iid and extra and xname in extra):
+          raise L.NotLowerable('norm density over data needs logpdf, iid=True '
+                               'and the data in extra')
+        return {'kind': 'norm_iid',
+                'obs': np.asarray(extra[xname], np.float64).reshape(-1),
+                'loc': names.index(slot['loc']),
+                'scale': names.index(slot['scale'])}, self._pscale(pscale_kw)
+      if len(names) != 1 or xname != names[0]:
+        raise L.NotLowerable('scipy density form needs a single variable')
+      loc, scale = np.array([float(loc)]), np.array([float(scale)])
+      if is_logpdf:
+        return {'kind': 'diag_gauss', 'mu': loc, 'sigma': scale}, \
+            self._pscale(pscale_kw)
+      if is_pdf:
+        return {'kind': 'norm_pdf', 'loc': loc, 'scale': scale}, \
+            self._pscale(pscale_kw)
+      return {'kind': 'uniform_pdf', 'lo': loc, 'scale': scale}, \
+          self._pscale(pscale_kw)
+    if callable(prob):
+      target, ps = L.trace_prob(prob, names)
+      return target, (self._pscale(pscale_kw) if pscale_kw else ps)
+    raise L.NotLowerable('density {} is not a recognised form'.format(prob))
+
+  def _tran_spec(self):
+    src = self._tran
+    if isinstance(src, RF):
+      src = src.tran
+    return src
+
+  def _delta_spec(self):
+    src = self._delta
+    if isinstance(src, RF):
+      return src.delta, src.delta_args, src.delta_kwds
+    return src if src is not None else (None, (), {})
+
+  def lower(self, extra=None, iid=False, joint=False):
+    """The kernel spec of this process (probayes_amd/spec.py)."""
+    from probayes_amd.spec import make_spec
+    if self._tfun is not None:
+      raise L.NotLowerable('user tfun Gibbs (set_tfun) has no kernel')
+    names, rvs = self.keylist, self.roots.rvs
+    d = len(names)
+    extra = {_key(k): v for k, v in (extra or {}).items()}
+    target, pscale = self._lower_target(extra, iid)
+    scores = self._scores
+    if scores not in MCMC_SAMPLERS:
+      raise L.NotLowerable('set_scores() to one of {}'.format(MCMC_SAMPLERS))
+    # metropolis_/hastings_ thresh and update are the same functions
+    # (sp_utils.py:30-37,67-72); gibbs pairs only with gibbs.
+    ok = ('gibbs',) if scores == 'gibbs' else ('metropolis', 'hastings')
+    if self._update not in (None,) + ok or self._thresh not in (None,) + ok:
+      raise L.NotLowerable('mixed scores/thresh/update samplers')
+    prior = None
+    if joint:
+      lens = [rv.length for rv in rvs]
+      nl = [-np.log(L_) if np.isfinite(L_) else -np.inf for L_ in lens]
+      logp = nl[0]
+      for v in nl[1:]:
+        logp = logp + v                               # prod_rule order
+      prior = {'lo': [rv.vlims[0] for rv in rvs],
+               'hi': [rv.vlims[1] for rv in rvs],
+               'lo_incl': [int(rv.lo_incl) for rv in rvs],
+               'hi_incl': [int(rv.hi_incl) for rv in rvs],
+               'logp': float(logp)}
+    ufun = [int(rv.log_ufun) for rv in rvs]
+    tran = self._tran_spec()
+    if scores == 'gibbs':
+      t, targs, tkw = tran if tran else (None, (), {})
+      if t is not scipy.stats.multivariate_normal or len(targs) < 2:
+        raise L.NotLowerable('gibbs needs set_tran(multivariate_normal, mean, '
+                             'cov, tsteps=...)')
+      proposal = {'kind': 'gibbs', 'mean': targs[0], 'cov': targs[1],
+                  'lo': [rv.vlims[0] for rv in rvs],
+                  'hi': [rv.vlims[1] for rv in rvs],
+                  'tsteps': int(tkw.get('tsteps') or 1)}
+      return make_spec(d, target, proposal, scores='gibbs', pscale=pscale,
+                       prior=prior, ufun=ufun, names=names)
+    proposal = self._lower_delta(rvs, names)
+    tran_spec = self._lower_tran(tran, names, scores)
+    return make_spec(d, target, proposal, scores=scores, pscale=pscale,
+                     tran=tran_spec, prior=prior, ufun=ufun, names=names)
+
+  def _lower_delta(self, rvs, names):
+    delta, dargs, dkw = self._delta_spec()
+    scale = bool(dkw.get('scale', False))
+    if dkw.get('bound', False):
+      raise L.NotLowerable('bound=True deltas have no kernel')
+    if dargs:
+      raise L.NotLowerable('per-variable unscaled deltas have no kernel')
+    lengths = np.array([rv.length for rv in rvs], np.float64)
+    if isinstance(delta, tuple):
+      if scale and not np.all(np.isfinite(lengths)):
+        raise ValueError('Cannot spherise variables with infinite length')
+      d0 = float(delta[0])
+      if scale:
+        d0 = d0 * np.sqrt(np.sum(lengths ** 2))        # field.py:513-515
+        mult = lengths
+      else:
+        mult = np.ones(len(rvs))
+      return {'kind': 'sphere', 'delta': d0, 'lengths': mult}
+    if isinstance(delta, list):
+      d0 = float(delta[0])
+      dv = d0 * lengths if scale else np.full(len(rvs), d0)
+      return {'kind': 'uniform', 'delta': dv}
+    if callable(delta):
+      return L.trace_delta(delta, names)
+    raise L.NotLowerable('delta {} has no kernel'.format(delta))
+
+  def _lower_tran(self, tran, names, scores):
+    if scores == 'metropolis':
+      return None
+    if not tran or tran[0] is None:
+      raise L.NotLowerable('hastings scores need set_tran()')
+    t = tran[0]
+    if isinstance(t, tuple):
+      form = L.trace_tran(t[0], names)
+      form['sym'] = False
+    else:
+      form = L.trace_tran(t, names)
+      form['sym'] = True
+    return form
+
+  # ---- sampling (sp.py:261-295) ---------------------------------------------
+  def sampler(self, *args, stop=None, iid=False, joint=False, chains=None,
+              seeds=None, rng=None, seed=0, device=0, thin=1,
+              steps_per_launch=0, debug=None):
+    init = args[0] if args else None
+    extra = args[1] if len(args) > 1 else None
+    if stop is None:
+      raise NotImplementedError('the GPU sampler needs stop=n_steps')
+    return Sampler(self, init, extra, int(stop), iid, joint, chains, seeds,
+                   rng, seed, device, thin, steps_per_launch, debug)
+
+  def walk(self, sampler, stop=None):
+    """sp.py:281-295."""
+    steps = collections.deque()
+    for sample in sampler:
+      if stop is not None and len(steps) >= stop:
+        break
+      steps.append(sample)
+    return steps
+
+  def __call__(self, samples, **kwds):
+    """Summary of a walk (sp.py:131-198) as trace-backed PDs."""
+    samples = list(samples)
+    if not samples or not isinstance(samples[0], Step):
+      raise TypeError('SP() summarises samples from SP.sampler()')
+    sm = samples[0].sampler
+    idx = np.array([s.i for s in samples])
+    return sm.summary(idx)
+
+
+OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',
+                                                'u', 'v'])
+
+
+class Step:
+  """One recorded step of a Sampler; fields as the reference's opqrstuv
+  (sp.py:257-258), built lazily from the trace arrays."""
+
+  __slots__ = ('sampler', 'i')
+
+  def __init__(self, sampler, i):
+    self.sampler, self.i = sampler, i
+
+  def _pd(self, xs, ps, t):
+    sm = self.sampler
+    vals = {k: xs[..., t, i] if sm.batched else float(xs[0, t, i])
+            for i, k in enumerate(sm.names)}
+    prob = ps[..., t] if sm.batched else float(ps[0, t])
+    return PD('p', vals, prob=prob, pscale=sm.pscale)
+
+  @property
+  def v(self):
+    return self._pd(self.sampler.tr['v_x'], self.sampler.tr['v_p'], self.i)
+
+  @property
+  def p(self):
+    tr = self.sampler.tr
+    if 'p_x' not in tr:
+      return None
+    return self._pd(tr['p_x'], tr['p_p'], self.i)
+
+  @property
+  def o(self):
+    if self.i == 0:
+      return None
+    return self._pd(self.sampler.tr['v_x'], self.sampler.tr['v_p'], self.i - 1)
+
+  @property
+  def u(self):
+    u = self.sampler.tr['u'][:, self.i].astype(bool)
+    if self.sampler.batched:
+      return u
+    return True if u[0] else None
+
+  @property
+  def s(self):
+    tr = self.sampler.tr
+    if 's' not in tr:
+      return None
+    v = tr['s'][:, self.i]
+    if self.sampler.batched:
+      return v
+    return None if np.isnan(v[0]) else float(v[0])
+
+  @property
+  def t(self):
+    th = self.sampler.thresholds
+    if th is None:
+      return None
+    return th[:, self.i] if self.sampler.batched else float(th[0, self.i])
+
+  def astuple(self):
+    return OPQRSTUV(self.o, self.p, None, None, self.s, self.t, self.u, self.v)
+
+  def __getitem__(self, i):
+    return self.astuple()[i]
+
+
+class Sampler:
+  """A lowered, batched MH/Gibbs run of `stop` steps (sp.py:261-278)."""
+
+  def __init__(self, sp, init, extra, stop, iid, joint, chains, seeds, rng,
+               seed, device, thin, steps_per_launch, debug):
+    self.sp, self.init, self.extra = sp, init, extra
+    self.stop, self.iid, self.joint = stop, iid, joint
+    self.batched = chains is not None
+    self.n = int(chains) if self.batched else 1
+    self.seeds = seeds
+    if rng is None:
+      rng = 'legacy' if (not self.batched or seeds is not None) else 'philox'
+    self.rng, self.seed, self.device = rng, seed, device
+    self.thin, self.spl = int(thin), int(steps_per_launch)
+    self.debug = (not self.batched) if debug is None else bool(debug)
+    self.names = sp.keylist
+    self.tr = None
+    self.thresholds = None
+    self.spec = None
+
+  def _init_array(self):
+    d, n = len(self.names), self.n
+    init = {_key(k): v for k, v in (self.init or {}).items()}
+    out = np.empty((n, d))
+    for i, k in enumerate(self.names):
+      if k not in init:
+        raise ValueError('init value missing for {}'.format(k))
+      out[:, i] = np.broadcast_to(np.asarray(init[k], np.float64), (n,))
+    return out
+
+  def run(self):
+    if self.tr is not None:
+      return self
+    self.spec = self.sp.lower(self.extra, self.iid, self.joint)
+    self.pscale = self.spec['pscale']
+    eng = Engine(self.spec, device=self.device)
+    try:
+      eng.init_chains(self._init_array())
+      if self.rng == 'legacy':
+        seeds = None if self.seeds is None else np.asarray(self.seeds)
+        if seeds is None and self.batched:
+          raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
+        streams = replay.legacy_streams(self.spec, self.stop, seeds)
+        eng.set_rng('replay')
+        eng.upload_replay(streams)
+        if self.spec['proposal']['kind'] != 'gibbs':
+          th = streams[:, -1, :].T
+          self.thresholds = th[:, self.thin - 1::self.thin]
+      else:
+        eng.set_rng(self.rng, self.seed)
+      eng.alloc_trace(self.stop // self.thin, self.thin, debug=self.debug)
+      eng.run(self.stop, steps_per_launch=self.spl)
+      self.tr = eng.trace()
+      self.moments = eng.moments()
+    finally:
+      eng.close()
+    return self
+
+  def __iter__(self):
+    self.run()
+    for t in range(self.tr['v_x'].shape[1]):
+      yield Step(self, t)
+
+  def summary(self, idx=None):
+    self.run()
+    T = self.tr['v_x'].shape[1]
+    idx = np.arange(T) if idx is None else np.asarray(idx)
+    sel = (lambda a: a[0, idx]) if not self.batched else \
+        (lambda a: np.moveaxis(a[:, idx], 0, 1))
+
+    def pd(xkey, pkey):
+      if xkey not in self.tr:
+        return None
+      xs = self.tr[xkey]
+      vals = {k: sel(xs[..., i]) for i, k in enumerate(self.names)}
+      return PD('p', vals, prob=sel(self.tr[pkey]), pscale=self.pscale)
+
+    u = sel(self.tr['u']).astype(bool)
+    if self.batched:
+      u = u.view(FlagArray)
+    else:
+      u = [True if b else None for b in u]
+    s = sel(self.tr['s']) if 's' in self.tr else None
+    t = None if self.thresholds is None else sel(self.thresholds)
+    v = pd('v_x', 'v_p')
+    return OPQRSTUV(None, pd('p_x', 'p_p'), None, None, s, t, u, v)

@@ -1,0 +1,234 @@
+"""The examples/mcmc workloads as builder functions of the API module `pb`.
+
+Each builder restates one reference script (cited per builder) with only the
+step counts and seeds changed.  `pb` is either the reference package (run by
+tools/gen_golden.py in the build container to record tests/golden/) or
+probayes_amd (run by the facade tests) -- the same code drives both, so the
+facade tests read like the reference's own example scripts.
+"""
+import numpy as np
+import scipy
+import scipy.stats
+import scipy.special
+
+
+# ----------------------------------------------------------------------------
+# Model builders.  Each returns (process, init, extra, sampler_kwds, keys)
+# ----------------------------------------------------------------------------
+def metrohast_norm1d(pb, params):
+  """examples/mcmc/metrohast_norm1d.py:13-40 (cfg1)."""
+  x_obs = params['x_obs']
+  mu = pb.RV('mu', vtype=float, vset=(40, 60), pscale='log')
+  sigma = pb.RV('sigma', vtype=float, vset=(5, 20.), pscale='log')
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  sigma.set_ufun((np.log, np.exp))
+  paras = pb.RF(mu, sigma)
+  stats = pb.RF(x)
+  process = pb.SP(stats, paras)
+  process.set_prob(scipy.stats.norm.logpdf,
+                   order={'x': 0, 'mu': 'loc', 'sigma': 'scale'})
+  tran = lambda **x: 1.
+  paras.set_tran((tran, tran))
+  paras.set_delta((0.005,), scale=True)
+  process.set_tran(paras)
+  process.set_delta(paras)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  init = {mu: 50., sigma: 12.5}
+  return process, init, {x: x_obs}, {'iid': True, 'joint': True}, ['mu', 'sigma']
+
+
+def mcmc_prob2(pb, params):
+  """examples/mcmc/mcmc_prob2.py:19-31."""
+  def q(**kwds):
+    x, xprime = kwds['x'], kwds["x'"]
+    return scipy.stats.norm.pdf(xprime, loc=x, scale=1.)
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x)
+  process.set_prob(scipy.stats.norm.pdf, loc=2, scale=np.sqrt(2),
+                   order={'x': 0})
+  process.set_tran(q)
+  lambda_delta = lambda: process.Delta(x=scipy.stats.norm.rvs(loc=0., scale=1.))
+  process.set_delta(lambda_delta)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 0.}, None, {}, ['x']
+
+
+def mcmc_prob3(pb, params):
+  """examples/mcmc/mcmc_prob3.py:27-39 (uniform target, linear pscale)."""
+  def q(**kwds):
+    x, xprime = kwds['x'], kwds["x'"]
+    return scipy.stats.norm.pdf(xprime, loc=x, scale=1.)
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x)
+  process.set_prob(scipy.stats.uniform.pdf, loc=3., scale=4.,
+                   order={'x': 0})
+  process.set_tran(q)
+  lambda_delta = lambda: process.Delta(x=scipy.stats.norm.rvs(loc=0., scale=1.))
+  process.set_delta(lambda_delta)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 5.}, None, {}, ['x']
+
+
+def _q2(prop_stdv, xoff=0.):
+  def q(**kwds):
+    x, xprime = kwds['x'], kwds["x'"]
+    y, yprime = kwds['y'], kwds["y'"]
+    return scipy.stats.norm.pdf(yprime, loc=y, scale=prop_stdv) * \
+           scipy.stats.norm.pdf(xprime, loc=x+xoff, scale=prop_stdv)
+  return q
+
+
+def mcmc_prob4a(pb, params):
+  """examples/mcmc/mcmc_prob4a.py:33-48 (2-D mvn target, permuted density)."""
+  prop_stdv = np.sqrt(1)
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x & y)
+  process.set_prob(scipy.stats.multivariate_normal, [0., 0.],
+                   [[2.0, 1.2], [1.2, 2.0]])
+  process.set_tran(_q2(prop_stdv))
+  lambda_delta = lambda: process.Delta(
+      x=scipy.stats.norm.rvs(loc=0., scale=prop_stdv),
+      y=scipy.stats.norm.rvs(loc=0., scale=prop_stdv))
+  process.set_delta(lambda_delta)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 0., 'y': 1.}, None, {}, ['x', 'y']
+
+
+def mcmc_prob4b(pb, params):
+  """examples/mcmc/mcmc_prob4b.py:31-51 (top-hat product target)."""
+  prop_stdv = np.sqrt(1)
+  def p(**kwds):
+    return scipy.stats.uniform.pdf(kwds['x'], loc=3., scale=4.) * \
+           scipy.stats.uniform.pdf(kwds['y'], loc=1., scale=8.)
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x & y)
+  process.set_prob(p)
+  process.set_tran(_q2(prop_stdv))
+  lambda_delta = lambda: process.Delta(
+      x=scipy.stats.norm.rvs(loc=0., scale=prop_stdv),
+      y=scipy.stats.norm.rvs(loc=0., scale=prop_stdv))
+  process.set_delta(lambda_delta)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 5., 'y': 5.}, None, {}, ['x', 'y']
+
+
+def mcmc_prob6(pb, params):
+  """examples/mcmc/mcmc_prob6.py:44-61 (asymmetric (q, r) tuple tran)."""
+  prop_stdv = np.sqrt(1)
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x & y)
+  process.set_prob(scipy.stats.multivariate_normal, [0., 0.],
+                   [[2.0, 1.2], [1.2, 2.0]])
+  process.set_tran((_q2(prop_stdv, 2.), _q2(prop_stdv, -2.)))
+  lambda_delta = lambda: process.Delta(
+      x=scipy.stats.norm.rvs(loc=-2, scale=prop_stdv),
+      y=scipy.stats.norm.rvs(loc=0., scale=prop_stdv))
+  process.set_delta(lambda_delta)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 0., 'y': 1.}, None, {}, ['x', 'y']
+
+
+def gibbs_norm2d(pb, params):
+  """examples/mcmc/gibbs_norm2d.py:9-21."""
+  lims = (-10., 10.)
+  means = [0.5, -0.5]
+  covar = [[1.5, -1.0], [-1.0, 2.]]
+  x = pb.RV('x', vtype=float, vset=lims)
+  y = pb.RV('y', vtype=float, vset=lims)
+  process = pb.SP(x & y)
+  process.set_prob(scipy.stats.multivariate_normal, means, covar)
+  process.set_tran(scipy.stats.multivariate_normal, means, covar, tsteps=1)
+  process.set_scores('gibbs')
+  return process, {'x': 0., 'y': 1.}, None, {}, ['x', 'y']
+
+
+def diag10(pb, params):
+  """10-dim diagonal Gaussian, callable N(0, 0.5^2) delta."""
+  mus, sigmas = params['mu'], params['sigma']
+  keys = ['x{}'.format(i) for i in range(len(mus))]
+  xs = [pb.RV(k, vtype=float, vset=(-np.inf, np.inf)) for k in keys]
+  process = pb.SP(pb.RF(*xs))
+  def lp(**kw):
+    return sum(scipy.stats.norm.logpdf(kw[k], mus[i], sigmas[i])
+               for i, k in enumerate(keys))
+  process.set_prob(lp, pscale='log')
+  process.set_tran(lambda **kw: 1.)
+  process.set_delta(lambda: process.Delta(
+      **{k: scipy.stats.norm.rvs(scale=params['step']) for k in keys}))
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {k: 0. for k in keys}, None, {}, keys
+
+
+def gibbs8(pb, params):
+  """8-dim mvn CondCov Gibbs."""
+  mean, cov = params['mean'], params['cov']
+  keys = ['x{}'.format(i) for i in range(len(mean))]
+  xs = [pb.RV(k, vtype=float, vset=(-20., 20.)) for k in keys]
+  process = pb.SP(pb.RF(*xs))
+  process.set_prob(scipy.stats.multivariate_normal, mean, cov)
+  process.set_tran(scipy.stats.multivariate_normal, mean, cov, tsteps=1)
+  process.set_scores('gibbs')
+  return process, {k: 0. for k in keys}, None, {}, keys
+
+
+def gmm2(pb, params):
+  """3-component 2-D isotropic Gaussian mixture."""
+  logw, mu, sd = np.log(params['w']), params['mu'], params['sd']
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x & y)
+  def logp(**kw):
+    a = logw + scipy.stats.norm.logpdf(kw['x'], mu[:, 0], sd) + \
+               scipy.stats.norm.logpdf(kw['y'], mu[:, 1], sd)
+    m = np.max(a)
+    return m + np.log(np.sum(np.exp(a - m)))
+  if hasattr(pb, 'models'):   # probayes_amd: the same density as a descriptor
+    logp = pb.models.GaussianMixtureLogPDF(['x', 'y'], params['w'], mu, sd)
+  process.set_prob(logp, pscale='log')
+  process.set_tran(lambda **kw: 1.)
+  step = params['step']
+  process.set_delta(lambda: process.Delta(
+      x=scipy.stats.norm.rvs(scale=step), y=scipy.stats.norm.rvs(scale=step)))
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 0., 'y': 0.}, None, {}, ['x', 'y']
+
+
+def _cfg3_params():
+  rs = np.random.RandomState(123)
+  A = rs.normal(size=(8, 8))
+  cov = A.dot(A.T) / 8 + 0.5 * np.eye(8)
+  mean = 0.5 * rs.normal(size=8)
+  return {'mean': mean, 'cov': cov}
+
+
+WORKLOADS = {
+  # name: (builder, params, n_chains, n_steps, seed0)
+  'metrohast_norm1d': (metrohast_norm1d,
+                       {'x_obs': np.random.RandomState(1).normal(50., 10., 60)},
+                       32, 256, 1000),
+  'mcmc_prob2': (mcmc_prob2, {}, 32, 256, 2000),
+  'mcmc_prob3': (mcmc_prob3, {}, 16, 256, 3000),
+  'mcmc_prob4a': (mcmc_prob4a, {}, 16, 256, 4000),
+  'mcmc_prob4b': (mcmc_prob4b, {}, 16, 256, 4500),
+  'mcmc_prob6': (mcmc_prob6, {}, 16, 256, 6000),
+  'gibbs_norm2d': (gibbs_norm2d, {}, 16, 256, 7000),
+  'diag10': (diag10, {'mu': np.linspace(-1., 1., 10),
+                      'sigma': np.linspace(0.5, 2., 10), 'step': 0.5},
+             32, 256, 8000),
+  'gibbs8': (gibbs8, _cfg3_params(), 16, 256, 9000),
+  'gmm2': (gmm2, {'w': np.array([0.3, 0.5, 0.2]),
+                  'mu': np.array([[-2., 0.], [2., 1.], [0., -2.5]]),
+                  'sd': np.array([0.6, 0.8, 0.5]), 'step': 0.7},
+           32, 256, 10000),
+}

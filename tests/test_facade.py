@@ -1,0 +1,131 @@
+"""The SP facade: the examples/mcmc scripts written against probayes_amd.
+
+CPU tests: every example lowers to exactly the workload spec the oracle was
+pinned with.  GPU tests: the example scripts run end to end on the engine and
+reproduce the reference's recorded chains -- one chain per sampler drawing
+from NumPy's GLOBAL legacy stream after np.random.seed (the reference's own
+convention), and all chains at once with chains=N, seeds=[...].
+"""
+import numpy as np
+import pytest
+
+import oracle
+import probayes_amd as pb
+from mcmc_examples import WORKLOADS
+
+
+def _spec_equal(a, b, path=''):
+  bad = []
+  if isinstance(a, dict):
+    if set(a) != set(b):
+      return [path + ':keys']
+    for k in a:
+      bad += _spec_equal(a[k], b[k], path + '.' + k)
+  elif isinstance(a, (np.ndarray, list, tuple)):
+    if not np.array_equal(np.asarray(a), np.asarray(b)):
+      bad.append(path)
+  elif a != b:
+    bad.append(path)
+  return bad
+
+
+def _build(name):
+  builder, params, n, t, seed0 = WORKLOADS[name]
+  g = oracle.load_golden(name)
+  params = oracle.workloads.golden_params(g) if params else params
+  process, init, extra, kwds, keys = builder(pb, params)
+  return process, init, extra, kwds, keys, g
+
+
+@pytest.mark.parametrize('name', sorted(WORKLOADS))
+def test_examples_lower_to_the_oracle_spec(name):
+  process, init, extra, kwds, keys, g = _build(name)
+  spec = process.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  ref = oracle.golden_spec(name, g)
+  for k in ('dim', 'pscale', 'scores', 'ufun', 'target', 'proposal', 'tran',
+            'prior'):
+    if spec['scores'] == 'gibbs' and k == 'tran':
+      continue
+    assert not _spec_equal(spec[k], ref[k]), (k, _spec_equal(spec[k], ref[k]))
+
+
+def test_unrecognised_forms_fail_loudly():
+  import scipy.stats
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x)
+  process.set_prob(lambda **kw: np.cos(kw['x']))
+  process.set_tran(lambda **kw: 1.)
+  process.set_delta(lambda: process.Delta(x=scipy.stats.norm.rvs()))
+  process.set_scores('hastings')
+  with pytest.raises(pb.NotLowerable):
+    process.lower()
+  process.set_prob(scipy.stats.norm.pdf, order={'x': 0})
+  process.set_delta(lambda: process.Delta(x=np.random.uniform()))
+  with pytest.raises(pb.NotLowerable):
+    process.lower()
+
+
+def _golden_rtol(a, b):
+  den = np.maximum(np.abs(b), 1.)
+  return float(np.max(np.abs(a - b) / den))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', sorted(WORKLOADS))
+def test_example_scripts_reproduce_reference_chains(name):
+  """np.random.seed(s); build; sampler; walk; SP(samples) -- as the reference
+  example scripts do -- gives the reference's recorded chain."""
+  builder, params, n, t, seed0 = WORKLOADS[name]
+  g = oracle.load_golden(name)
+  for c in range(2):
+    process, init, extra, kwds, keys, _ = _build(name)
+    np.random.seed(int(g['seeds'][c]))
+    args = (init,) if extra is None else (init, extra)
+    sampler = process.sampler(*args, stop=t, **kwds)
+    samples = process.walk(sampler)
+    summary = process(samples)
+    for i, k in enumerate(keys):
+      assert _golden_rtol(np.asarray(summary.v[k]), g['v_x'][c, :, i]) <= 1e-12
+    assert _golden_rtol(np.asarray(summary.v.prob), g['v_p'][c]) <= 1e-12
+    assert summary.u.count(True) == int(g['u'][c].sum())
+    # the global legacy stream advanced exactly as the reference's did
+    rs = np.random.RandomState(int(g['seeds'][c]))
+    oracle.legacy_streams  # (documentation: same consumption order)
+    d = len(keys)
+    for _ in range(t):
+      if name.startswith('gibbs'):
+        rs.random_sample()
+      elif name == 'metrohast_norm1d':
+        rs.random_sample(d); rs.random_sample()
+      else:
+        rs.standard_normal(d); rs.random_sample()
+    assert np.random.random_sample() == rs.random_sample()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['metrohast_norm1d', 'diag10', 'gibbs8',
+                                  'gmm2', 'mcmc_prob6'])
+def test_batched_sampler_reproduces_all_reference_chains(name):
+  builder, params, n, t, seed0 = WORKLOADS[name]
+  process, init, extra, kwds, keys, g = _build(name)
+  args = (init,) if extra is None else (init, extra)
+  sampler = process.sampler(*args, stop=t, chains=n, seeds=g['seeds'], **kwds)
+  summary = process(process.walk(sampler))
+  for i, k in enumerate(keys):
+    got = np.asarray(summary.v[k]).T            # [N, T]
+    assert _golden_rtol(got, g['v_x'][:, :, i]) <= 1e-12
+  assert summary.u.count(True) == int(g['u'].sum())
+
+
+@pytest.mark.gpu
+def test_batched_philox_sampler_posterior():
+  """metrohast_norm1d posterior with 4096 production chains."""
+  process, init, extra, kwds, keys, g = _build('metrohast_norm1d')
+  sampler = process.sampler(init, extra, stop=2000, chains=4096, rng='philox',
+                            seed=7, **kwds)
+  summary = process(process.walk(sampler))
+  mus = np.asarray(summary.v['mu'])[500:]
+  sig = np.asarray(summary.v['sigma'])[500:]
+  x = g['param_x_obs']
+  assert abs(np.mean(mus) - np.mean(x)) < 0.5
+  assert abs(np.median(sig) - np.std(x)) < 1.5

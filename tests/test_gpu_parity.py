@@ -181,3 +181,22 @@ def test_engine_errors_are_loud():
   eng.run(4)
   assert eng.trace_len() == 4
   eng.close()
+
+
+def test_rccl_single_rank_allgather_and_max():
+  """The engine's RCCL path (one rank: the GPU box has one card)."""
+  from probayes_amd import Engine
+  spec = _diag10_spec()
+  eng = Engine(spec)
+  eng.init_chains(np.zeros((1000, 10)))
+  eng.set_rng('philox', 3)
+  eng.run(20)
+  eng.rccl_init(0, 1, Engine.rccl_unique_id())
+  g = eng.rccl_allgather_moments()
+  m = eng.moments()
+  assert g.shape == (1, 21, 1000)
+  np.testing.assert_array_equal(g[0, :10].T, m['sum'])
+  np.testing.assert_array_equal(g[0, 10:20].T, m['sumsq'])
+  np.testing.assert_array_equal(g[0, 20], m['n_acc'])
+  assert eng.rccl_allreduce_max(2.5) == 2.5
+  eng.close()
