@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,6 +51,7 @@ struct pbh_engine {
   double *msum = nullptr, *msq = nullptr;
   int64_t *nacc = nullptr;
   int64_t mom_steps = 0;
+  bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   // timing of the last pbh_run
   bool timed = false;
   int64_t last_launches = 0;
@@ -163,6 +165,7 @@ int pbh_create(int device, pbh_engine **out) {
   HIP_TRY(hipSetDevice(device));
   pbh_engine *e = new pbh_engine();
   e->device = device;
+  if (const char *np = std::getenv("PBH_NO_PAIR")) e->pair_enabled = np[0] != '1';
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -538,6 +541,15 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.rec_cap = e->cap;
   k.debug = e->debug;
   k.W = (e->n + 63) / 64;
+  {
+    // The lane-pair kernel drops the per-step tran evaluation: allowed when
+    // the constant tran's rescaled value q~ > 0 (sp_utils.py:52-54 never
+    // returns None); see pair_form in pbh_kernels_impl.h.
+    const double v = k.tran_value;
+    const double qt = k.pscale == PBH_PSCALE_LIN
+                          ? v : (v <= k.log_npi ? std::exp(v) : 1.7976931348623158e+308);
+    k.pair_ok = (e->pair_enabled && (k.scores == PBH_SCORES_METROPOLIS || qt > 0.0)) ? 1 : 0;
+  }
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384)
                          ? (size_t)k.tn * sizeof(double) : 0;

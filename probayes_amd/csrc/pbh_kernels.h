@@ -54,6 +54,7 @@ struct KArgs {
   int64_t rec_cap;
   int32_t debug;
   int64_t W;         // accept-mask words per recorded step = ceil(n / 64)
+  int32_t pair_ok;   // engine allows the lane-pair kernel (see launch_mh_d)
   // ---- moments ----
   double *msum, *msq;
   int64_t *nacc;

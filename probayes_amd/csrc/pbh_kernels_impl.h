@@ -24,6 +24,14 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// Model constants are never written by a kernel: reading them through the
+// constant address space lets the compiler use scalar loads (s_load) with
+// wave-uniform addresses and hoist them, instead of per-step vector loads
+// that it must assume alias the trace stores.
+__device__ __forceinline__ double cld(const double *p, int64_t i) {
+  return ((const __attribute__((address_space(4))) double *)p)[i];
+}
+
 // prob.py:354-357: the mvn density is evaluated at the values reversed and,
 // for d > 2, rotated by one: [x_{d-2}, ..., x_0, x_{d-1}] (App. A-4).
 template <int D>
@@ -70,17 +78,17 @@ __device__ __forceinline__ double mvn_density(const KArgs &a,
   // -0.5 * (rank*log(2pi) + log_pdet + maha); pdf = exp(logpdf).
   double dev[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) dev[i] = x[mvn_perm<D>(i)] - a.ta[i];
+  for (int i = 0; i < D; ++i) dev[i] = x[mvn_perm<D>(i)] - cld(a.ta, i);
   double sq[D];
 #pragma unroll
   for (int j = 0; j < D; ++j) {
-    double y = dev[0] * a.tb[j];
+    double y = dev[0] * cld(a.tb, j);
 #pragma unroll
-    for (int i = 1; i < D; ++i) y = y + dev[i] * a.tb[i * D + j];
+    for (int i = 1; i < D; ++i) y = y + dev[i] * cld(a.tb, i * D + j);
     sq[j] = y * y;
   }
   const double maha = np_sum_regs<D>(sq, D);
-  const double logpdf = -0.5 * (a.tc[0] + maha);
+  const double logpdf = -0.5 * (cld(a.tc, 0) + maha);
   return a.pscale == PBH_PSCALE_LIN ? exp(logpdf) : logpdf;
 }
 
@@ -97,13 +105,13 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
         // production path: FMA-corrected division by the constant sigma
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          const double y = div_by(x[k] - a.ta[k], a.tb[k], a.te[k]);
-          out = out + (((y * y) * -0.5 - a.norm_logC) - a.tc[k]);
+          const double y = div_by(x[k] - cld(a.ta, k), cld(a.tb, k), cld(a.te, k));
+          out = out + (((y * y) * -0.5 - a.norm_logC) - cld(a.tc, k));
         }
       } else {
 #pragma unroll
         for (int k = 0; k < D; ++k)
-          out = out + norm_logpdf(x[k], a.ta[k], a.tb[k], a.tc[k], a.norm_logC);
+          out = out + norm_logpdf(x[k], cld(a.ta, k), cld(a.tb, k), cld(a.tc, k), a.norm_logC);
       }
       break;
     }
@@ -132,10 +140,10 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
       // a_k = logw_k + sum_i logpdf(x_i, mu_ki, sd_k); m + log(sum exp(a - m))
       const int64_t K = a.tn;
       auto comp = [&](int64_t k) {
-        double v = a.ta[k];
+        double v = cld(a.ta, k);
 #pragma unroll
         for (int i = 0; i < D; ++i)
-          v = v + norm_logpdf(x[i], a.tb[k * D + i], a.tc[k], a.te[k],
+          v = v + norm_logpdf(x[i], cld(a.tb, k * D + i), cld(a.tc, k), cld(a.te, k),
                               a.norm_logC);
         return v;
       };
@@ -149,16 +157,16 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
       break;
     }
     case PBH_TARGET_NORM_PDF: {
-      out = norm_pdf(x[0], a.ta[0], a.tb[0], a.norm_C);
+      out = norm_pdf(x[0], cld(a.ta, 0), cld(a.tb, 0), a.norm_C);
 #pragma unroll
       for (int k = 1; k < D; ++k)
-        out = out * norm_pdf(x[k], a.ta[k], a.tb[k], a.norm_C);
+        out = out * norm_pdf(x[k], cld(a.ta, k), cld(a.tb, k), a.norm_C);
       break;
     }
     case PBH_TARGET_UNIFORM_PDF: {
-      out = uniform_pdf(x[0], a.ta[0], a.tb[0]);
+      out = uniform_pdf(x[0], cld(a.ta, 0), cld(a.tb, 0));
 #pragma unroll
-      for (int k = 1; k < D; ++k) out = out * uniform_pdf(x[k], a.ta[k], a.tb[k]);
+      for (int k = 1; k < D; ++k) out = out * uniform_pdf(x[k], cld(a.ta, k), cld(a.tb, k));
       break;
     }
     case PBH_TARGET_MVN:
@@ -173,10 +181,10 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
     bool inside = true;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      const bool lo_ok = ((a.plo_incl >> k) & 1u) ? (x[k] >= a.plo[k])
-                                                   : (x[k] > a.plo[k]);
-      const bool hi_ok = ((a.phi_incl >> k) & 1u) ? (x[k] <= a.phi[k])
-                                                   : (x[k] < a.phi[k]);
+      const bool lo_ok = ((a.plo_incl >> k) & 1u) ? (x[k] >= cld(a.plo, k))
+                                                   : (x[k] > cld(a.plo, k));
+      const bool hi_ok = ((a.phi_incl >> k) & 1u) ? (x[k] <= cld(a.phi, k))
+                                                   : (x[k] < cld(a.phi, k));
       inside = inside && lo_ok && hi_ok;
     }
     out = (inside ? a.prior_logp : kNearlyNegInf) + out;
@@ -221,7 +229,7 @@ __device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
       double v = 0.;
 #pragma unroll
       for (int kk = 0; kk < D; ++kk)
-        if (kk == k) v = norm_pdf(xp[kk], x[kk] + a.tran_off[kk], a.tran_scale, a.norm_C);
+        if (kk == k) v = norm_pdf(xp[kk], x[kk] + cld(a.tran_off, kk), a.tran_scale, a.norm_C);
       q = first ? v : q * v;
       first = false;
     }
@@ -261,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   bool use_lds = false;
   if ((TGT == 0 || TGT == PBH_TARGET_NORM_IID) &&
       a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
-    for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = a.ta[j];
+    for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = cld(a.ta, j);
     __syncthreads();
     use_lds = true;
   }
@@ -339,12 +347,12 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       if (prop == PBH_PROP_GAUSS) {
         // scipy rv_generic.rvs: z * scale + loc
 #pragma unroll
-        for (int k = 0; k < D; ++k) dl[k] = r[k] * a.pscl[k] + a.ploc[k];
+        for (int k = 0; k < D; ++k) dl[k] = r[k] * cld(a.pscl, k) + cld(a.ploc, k);
       } else if (prop == PBH_PROP_UNIFORM) {
         // np.random.uniform(-delta, delta) = low + (high - low) * u
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          const double d0 = a.pdel[k];
+          const double d0 = cld(a.pdel, k);
           dl[k] = -d0 + (d0 - -d0) * r[k];
         }
       } else {
@@ -359,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         const double ss = np_sum_regs<D>(sq, D);
         const double rss = ss >= kNearlyPosZero ? sqrt(ss) : 0.;
 #pragma unroll
-        for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * a.plen[k];
+        for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * cld(a.plen, k);
       }
 #pragma unroll
       for (int k = 0; k < D; ++k)
@@ -422,6 +430,187 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Lane-pair MH kernel for the sum-of-terms diagonal Gaussian with the
+// callable Gaussian delta (cfg2).  One chain per LANE PAIR (l, l + 32): lane
+// half h owns dims [h*H, h*H + H), H = D/2, so 65 536 chains fill 2 048
+// wavefronts = 2 per SIMD (the single-wave VALU issue limit halves throughput
+// at 1 wave/SIMD, MI355X_MICROARCH.md constants table).  The density keeps the
+// reference's left-to-right Python sum: half 0 sums its terms from 0 and hands
+// the partial to half 1 through v_permlane32_swap, half 1 finishes the sum,
+// scores, thresholds and hands the accept bit back.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t swap_u32(uint32_t v, bool hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return hi ? r[0] : r[1];
+}
+
+__device__ __forceinline__ double swap_f64(double v, bool hi) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint64_t lo = swap_u32((uint32_t)u, hi);
+  const uint64_t up = swap_u32((uint32_t)(u >> 32), hi);
+  return __builtin_bit_cast(double, lo | (up << 32));
+}
+
+template <int D, int RNG>
+__global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
+  static_assert(D % 2 == 0, "lane-pair kernel needs even D");
+  constexpr int H = D / 2;
+  constexpr bool FAST = RNG == PBH_RNG_PHILOX;
+  const bool lin = a.pscale == PBH_PSCALE_LIN;
+  const int lane = threadIdx.x & 63;
+  const bool hi = lane >= 32;
+  const int h = hi ? 1 : 0;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t c = wave * 32 + (lane & 31);
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int k0 = h * H;   // first dim of this half
+
+  double x[H], ms[H], mq[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    x[i] = a.x[(k0 + i) * a.n + cc];
+    ms[i] = 0.;
+    mq[i] = 0.;
+  }
+  double lp = a.lp[cc];
+  double eB = lin ? lp : exp_logp(lp, a.log_npi);
+  int64_t nacc = 0;
+  const int64_t chain = a.off + cc;
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const int64_t g = a.g0 + s;
+    double r[H];
+    double thr = 0.;
+    if (RNG == PBH_RNG_REPLAY) {
+      const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
+#pragma unroll
+      for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
+      if (hi) thr = row[(int64_t)D * a.n];
+    } else if (FAST) {
+      // per half: ceil(H/2) normal pairs, two pairs per Philox block
+      constexpr int P = (H + 1) / 2;
+#pragma unroll
+      for (int q = 0; q < (P + 1) / 2; ++q) {
+        const u32x4 w = philox4x32_10(ctr(q + 16 * h, g, chain), a.seed_lo, a.seed_hi);
+        double z1;
+        const double z0 = fast_normal_pair(w.x, w.z, z1);
+        if (4 * q < H) r[4 * q] = z0;
+        if (4 * q + 1 < H) r[4 * q + 1] = z1;
+        if (2 * q + 1 < P) {
+          double z3;
+          const double z2 = fast_normal_pair(w.y, w.w, z3);
+          if (4 * q + 2 < H) r[4 * q + 2] = z2;
+          if (4 * q + 3 < H) r[4 * q + 3] = z3;
+        } else {
+          thr = u01(w.y, w.w);   // spare half-block (used by half 1)
+        }
+      }
+      if (P % 2 == 0 && hi) {
+        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+        thr = u01(w.x, w.y);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < (H + 1) / 2; ++p) {
+        double z0, z1;
+        box_muller(philox4x32_10(ctr(p + 16 * h, g, chain), a.seed_lo, a.seed_hi), z0, z1);
+        r[2 * p] = z0;
+        if (2 * p + 1 < H) r[2 * p + 1] = z1;
+      }
+      if (hi) {
+        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+        thr = u01(w.x, w.y);
+      }
+    }
+    // proposal of this half's dims (scipy rvs: z * scale + loc)
+    double xp[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i)
+      xp[i] = x[i] + (r[i] * cld(a.pscl, k0 + i) + cld(a.ploc, k0 + i));
+    // density: Python sum from 0, dims in order, split across the pair
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      double t;
+      if (FAST) {
+        const double y = div_by(xp[i] - cld(a.ta, k0 + i), cld(a.tb, k0 + i),
+                                cld(a.te, k0 + i));
+        t = ((y * y) * -0.5 - a.norm_logC) - cld(a.tc, k0 + i);
+      } else {
+        t = norm_logpdf(xp[i], cld(a.ta, k0 + i), cld(a.tb, k0 + i),
+                        cld(a.tc, k0 + i), a.norm_logC);
+      }
+      r[i] = t;    // reuse r for the terms
+    }
+    double s0 = 0.0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) s0 = s0 + (hi ? 0.0 : r[i]);
+    const double from_lo = swap_f64(s0, hi);      // half 1 receives half 0's sum
+    double lpp = from_lo;
+#pragma unroll
+    for (int i = 0; i < H; ++i) lpp = lpp + r[i];
+    // only half 1's lpp is the full density; score there
+    uint32_t acc_bit = 0;
+    double eA = 0.;
+    if (hi) {
+      eA = lin ? lpp : exp_logp(lpp, a.log_npi);
+      bool acc;
+      if (!a.has_pred && s == 0) {
+        acc = true;
+      } else {
+        double q = eA / np_max_tiny(eB);
+        q = q < 1. ? q : 1.;
+        acc = q >= thr;
+      }
+      acc_bit = acc ? 1u : 0u;
+    }
+    const uint32_t acc_lo = swap_u32(acc_bit, hi);   // half 0 receives it
+    const bool acc = (hi ? acc_bit : acc_lo) != 0;
+    if (acc) {
+#pragma unroll
+      for (int i = 0; i < H; ++i) x[i] = xp[i];
+      if (hi) {
+        lp = lpp;
+        eB = eA;
+      }
+    }
+    nacc += acc ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      ms[i] += x[i];
+      mq[i] += x[i] * x[i];
+    }
+    if ((g + 1) % a.thin == 0) {
+      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+      if (rec >= 0 && rec < a.rec_cap) {
+        if (active) {
+#pragma unroll
+          for (int i = 0; i < H; ++i) a.tx[(rec * D + k0 + i) * a.n + c] = x[i];
+          if (hi) a.tlp[rec * a.n + c] = lp;
+        }
+        // 32 chains per wave: the upper half's ballot bits are the mask word
+        const uint64_t mask = __ballot(active && acc && hi) >> 32;
+        if (lane == 32 && (c >> 5) < 2 * a.W)
+          reinterpret_cast<uint32_t *>(a.tacc)[rec * 2 * a.W + (c >> 5)] =
+              (uint32_t)mask;
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      a.x[(k0 + i) * a.n + c] = x[i];
+      a.msum[(k0 + i) * a.n + c] += ms[i];
+      a.msq[(k0 + i) * a.n + c] += mq[i];
+    }
+    if (hi) {
+      a.lp[c] = lp;
+      a.nacc[c] += nacc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // CondCov Gibbs kernel (cond_cov.py:42-65 per coordinate; rf.py:446-458
 // cycling).  One SP step updates tsteps coordinates; u is always True.
 // ---------------------------------------------------------------------------
@@ -465,14 +654,14 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
         for (int i = 0; i < D; ++i) {
           if (i == k) continue;
           const int jj = i < k ? i : i - 1;
-          const double t = a.gcoef[k * (D - 1) + jj] * (x[i] - a.gmean[i]);
+          const double t = cld(a.gcoef, k * (D - 1) + jj) * (x[i] - cld(a.gmean, i));
           dot = first ? t : dot + t;
           first = false;
         }
-        const double lo = a.gcdf[2 * k], hi = a.gcdf[2 * k + 1];
+        const double lo = cld(a.gcdf, 2 * k), hi = cld(a.gcdf, 2 * k + 1);
         const double cdf = lo + (hi - lo) * u;     // np.random.uniform(lo, hi)
-        const double m = a.gmean[k] + dot;
-        x[k] = ndtri(cdf) * a.gstdv[k] + m;        // norm.ppf(cdf, m, sd)
+        const double m = cld(a.gmean, k) + dot;
+        x[k] = ndtri(cdf) * cld(a.gstdv, k) + m;        // norm.ppf(cdf, m, sd)
       }
     }
     lp = mvn_density<D>(a, x);
@@ -530,7 +719,35 @@ void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
 }
 
 template <int D>
+void launch_mh_pair(const KArgs &a, hipStream_t st) {
+  const int64_t waves = (a.n + 31) / 32;
+  const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
+  if (a.rng == PBH_RNG_REPLAY)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_REPLAY>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_PHILOX)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_F64>), grid, block, 0, st, a);
+}
+
+// The lane-pair kernel covers the cfg2 form: diagonal Gaussian, callable
+// Gaussian delta, no ufun / prior, symmetric tran or metropolis, debug off.
+inline bool pair_form(const KArgs &a) {
+  return a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS &&
+         a.ufun == 0 && !a.has_prior && !a.debug &&
+         (a.scores == PBH_SCORES_METROPOLIS ||
+          (a.scores == PBH_SCORES_HASTINGS && a.tran_sym &&
+           a.tran_kind == PBH_TRAN_CONST));
+}
+
+template <int D>
 hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
+  if constexpr (D % 2 == 0 && D >= 4) {
+    if (pair_form(a) && a.pair_ok) {
+      launch_mh_pair<D>(a, st);
+      return hipGetLastError();
+    }
+  }
   // Specialised forms: the cfg2 diagonal Gaussian with the callable Gaussian
   // delta at every d; the other example forms at the small d they use.
   if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS) {

@@ -200,3 +200,24 @@ def test_rccl_single_rank_allgather_and_max():
   np.testing.assert_array_equal(g[0, 20], m['n_acc'])
   assert eng.rccl_allreduce_max(2.5) == 2.5
   eng.close()
+
+
+@pytest.mark.parametrize('n', [32, 100])
+def test_lane_pair_kernel_replay_matches_reference(n):
+  """The cfg2 form without debug records runs the lane-pair kernel (one chain
+  per lanes l, l+32); it must reproduce the reference golden chains too,
+  including ragged chain counts."""
+  g = oracle.load_golden('diag10')
+  spec = oracle.golden_spec('diag10', g)
+  t = g['v_x'].shape[1]
+  seeds = np.concatenate([g['seeds'], np.arange(90000, 90000 + n - 32)])
+  streams = oracle.legacy_streams(spec, seeds, t)
+  out, mom = _run_replay(spec, golden_init('diag10', n), streams, debug=False)
+  ref = oracle.run_mh(spec, golden_init('diag10', n), streams)
+  assert np.array_equal(out['u'], ref['u'])
+  assert np.array_equal(out['u'][:32], g['u'])
+  assert _rel_err(out['v_x'], ref['v_x'], 1.) <= RTOL
+  assert _rel_err(out['v_p'], ref['v_p']) <= RTOL
+  assert np.array_equal(mom['n_acc'], ref['u'].sum(axis=1))
+  np.testing.assert_allclose(mom['sum'], ref['v_x'].sum(axis=1), rtol=1e-9,
+                             atol=1e-9)
