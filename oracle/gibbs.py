@@ -29,7 +29,7 @@ def condcov_tables(mean, cov, lo, hi):
     ru = np.delete(cov[i, :].reshape([1, n]), (i), axis=1)
     c = np.delete(np.delete(cov, (i), axis=1), (i), axis=0)
     coef.append(ru.dot(np.linalg.inv(c)))
-    stdv[i] = np.sqrt(cov[i, i] - float(coef[i].dot(ll)))
+    stdv[i] = np.sqrt(cov[i, i] - coef[i].dot(ll).item())
   cdfs = np.array([scipy.stats.norm.cdf(lim, loc=0., scale=stdv[i])
                    for i, lim in enumerate(lims)])
   return coef, stdv, cdfs
@@ -62,7 +62,7 @@ def run_gibbs(spec, init, streams):
         lims = cdfs[key]
         u = streams[t, 0, c]
         cdf = lims[0] + (lims[1] - lims[0]) * u     # legacy uniform(lo, hi)
-        m = mean[key] + float(coef[key].dot(dmu))
+        m = mean[key] + coef[key].dot(dmu).item()   # float(1x1 array)
         xc[key] = scipy.stats.norm.ppf(cdf, loc=m, scale=stdv[key])
       cond_mod += tsteps
       if cond_mod >= d:

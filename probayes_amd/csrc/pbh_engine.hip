@@ -239,6 +239,21 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
                 m->target_kind);
   oa = pack(blk, A, na); ob = pack(blk, B, nb); oc = pack(blk, C, nc);
   oe = pack(blk, E, ne);
+  // Production-path (PBH_RNG_PHILOX) diagonal-Gauss constants: w = sqrt(.5)
+  // / sigma and ksum = sum(logC + log sigma), so the density is
+  // -sum (w (x - mu))^2 - ksum: three fp64 ops per dim.  Parity modes use
+  // the reference's expression instead.
+  size_t ow = 0;
+  double ksum = 0.;
+  if (m->target_kind == PBH_TARGET_DIAG_GAUSS) {
+    std::vector<double> w(d);
+    const double logC = std::log(std::sqrt(2 * M_PI));
+    for (int i = 0; i < d; ++i) {
+      w[i] = std::sqrt(0.5) / B[i];
+      ksum += logC + C[i];
+    }
+    ow = pack(blk, w.data(), d);
+  }
   uint32_t lo_incl = 0, hi_incl = 0, ufun = 0;
   if (m->has_prior) {
     if (!m->prior_lo || !m->prior_hi || !m->prior_lo_incl || !m->prior_hi_incl)
@@ -279,6 +294,7 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
   const double *base = e->dmodel;
   k.d = d; k.target = m->target_kind; k.pscale = m->pscale; k.scores = m->scores;
   k.ta = base + oa; k.tb = base + ob; k.tc = base + oc; k.te = base + oe;
+  k.tw = base + ow; k.ksum = ksum;
   k.tn = (m->target_kind == PBH_TARGET_NORM_IID || m->target_kind == PBH_TARGET_GMM) ? m->n : 0;
   k.i0 = m->i0; k.i1 = m->i1;
   k.has_prior = m->has_prior ? 1 : 0;

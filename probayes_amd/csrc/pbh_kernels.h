@@ -30,6 +30,8 @@ struct KArgs {
   const double *gmean, *gcoef, *gstdv, *gcdf;
   int32_t tsteps;
   // ---- host-evaluated constants (bit-identical to the reference's) ----
+  const double *tw;  // DIAG_GAUSS production path: sqrt(0.5) / sigma
+  double ksum;       // DIAG_GAUSS production path: sum(logC + log sigma)
   double log_npi;    // np.log(NEARLY_POSITIVE_INF)
   double norm_logC;  // np.log(np.sqrt(2*np.pi))
   double norm_C;     // np.sqrt(2*np.pi)

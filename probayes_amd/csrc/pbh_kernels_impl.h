@@ -102,12 +102,13 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
     case PBH_TARGET_DIAG_GAUSS: {
       // lp(**kw) = sum(norm.logpdf(kw[k], mu_k, sigma_k)): Python sum from 0
       if (FAST) {
-        // production path: FMA-corrected division by the constant sigma
+        // production path: -sum_k (w_k (x_k - mu_k))^2 - ksum, w = sqrt(.5)/sigma
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          const double y = div_by(x[k] - cld(a.ta, k), cld(a.tb, k), cld(a.te, k));
-          out = out + (((y * y) * -0.5 - a.norm_logC) - cld(a.tc, k));
+          const double u = (x[k] - cld(a.ta, k)) * cld(a.tw, k);
+          out = __builtin_fma(-u, u, out);
         }
+        out = out - a.ksum;
       } else {
 #pragma unroll
         for (int k = 0; k < D; ++k)
@@ -529,26 +530,30 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     for (int i = 0; i < H; ++i)
       xp[i] = x[i] + (r[i] * cld(a.pscl, k0 + i) + cld(a.ploc, k0 + i));
     // density: Python sum from 0, dims in order, split across the pair
+    double lpp;
+    if (FAST) {
+      // production path: each half sums -(w (x - mu))^2 over its dims; the
+      // order of the fp64 sum is free here (no reference stream to match)
+      double part = 0.0;
 #pragma unroll
-    for (int i = 0; i < H; ++i) {
-      double t;
-      if (FAST) {
-        const double y = div_by(xp[i] - cld(a.ta, k0 + i), cld(a.tb, k0 + i),
-                                cld(a.te, k0 + i));
-        t = ((y * y) * -0.5 - a.norm_logC) - cld(a.tc, k0 + i);
-      } else {
-        t = norm_logpdf(xp[i], cld(a.ta, k0 + i), cld(a.tb, k0 + i),
-                        cld(a.tc, k0 + i), a.norm_logC);
+      for (int i = 0; i < H; ++i) {
+        const double u = (xp[i] - cld(a.ta, k0 + i)) * cld(a.tw, k0 + i);
+        part = __builtin_fma(-u, u, part);
       }
-      r[i] = t;    // reuse r for the terms
+      lpp = (part + swap_f64(part, hi)) - a.ksum;
+    } else {
+#pragma unroll
+      for (int i = 0; i < H; ++i)
+        r[i] = norm_logpdf(xp[i], cld(a.ta, k0 + i), cld(a.tb, k0 + i),
+                           cld(a.tc, k0 + i), a.norm_logC);  // terms
+      double s0 = 0.0;
+#pragma unroll
+      for (int i = 0; i < H; ++i) s0 = s0 + (hi ? 0.0 : r[i]);
+      const double from_lo = swap_f64(s0, hi);   // half 1 gets half 0's sum
+      lpp = from_lo;
+#pragma unroll
+      for (int i = 0; i < H; ++i) lpp = lpp + r[i];
     }
-    double s0 = 0.0;
-#pragma unroll
-    for (int i = 0; i < H; ++i) s0 = s0 + (hi ? 0.0 : r[i]);
-    const double from_lo = swap_f64(s0, hi);      // half 1 receives half 0's sum
-    double lpp = from_lo;
-#pragma unroll
-    for (int i = 0; i < H; ++i) lpp = lpp + r[i];
     // only half 1's lpp is the full density; score there
     uint32_t acc_bit = 0;
     double eA = 0.;

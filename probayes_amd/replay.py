@@ -48,6 +48,22 @@ def stream_width(spec):
   return int(spec['dim']) + 1
 
 
+def _chunk(args):
+  spec, n_steps, seeds, step0 = args
+  return legacy_streams(spec, n_steps, seeds, step0)
+
+
+def legacy_streams_parallel(spec, n_steps, seeds, processes=8, step0=0):
+  """legacy_streams over a process pool (chains are independent); used to
+  feed full-size replay runs (65 536 chains) in seconds."""
+  import multiprocessing as mp
+  seeds = np.asarray(seeds).reshape(-1)
+  chunks = np.array_split(seeds, max(1, min(processes, seeds.size)))
+  with mp.get_context('fork').Pool(len(chunks)) as pool:
+    parts = pool.map(_chunk, [(spec, n_steps, c, step0) for c in chunks])
+  return np.concatenate(parts, axis=2)
+
+
 def legacy_streams(spec, n_steps, seeds=None, step0=0):
   """[T, R, N] streams; seeds=None draws ONE chain from the global state."""
   d, kind = int(spec['dim']), spec['proposal']['kind']

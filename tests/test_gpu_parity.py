@@ -221,3 +221,26 @@ def test_lane_pair_kernel_replay_matches_reference(n):
   assert np.array_equal(mom['n_acc'], ref['u'].sum(axis=1))
   np.testing.assert_allclose(mom['sum'], ref['v_x'].sum(axis=1), rtol=1e-9,
                              atol=1e-9)
+
+
+def test_full_size_cfg2_replay_parity():
+  """BASELINE cfg2 at full width (65 536 chains): the GPU runs the
+  reference's own per-chain legacy streams; 256 sampled chains must match
+  the oracle step for step, and size-independent invariants hold for all
+  chains (trace accept bits == in-kernel accept counts, trace sums ==
+  in-kernel moments, every chain moved on step 1)."""
+  from probayes_amd.replay import legacy_streams_parallel
+  spec = oracle.golden_spec('diag10')
+  n, t = 65536, 120
+  seeds = np.arange(n, dtype=np.int64) + 7_000_000
+  streams = legacy_streams_parallel(spec, t, seeds, processes=16)
+  out, mom = _run_replay(spec, np.zeros((n, 10)), streams, debug=False)
+  assert np.array_equal(mom['n_acc'], out['u'].sum(axis=1))
+  np.testing.assert_allclose(mom['sum'], out['v_x'].sum(axis=1), rtol=1e-12,
+                             atol=1e-9)
+  assert out['u'][:, 0].all()
+  pick = np.random.RandomState(5).choice(n, 256, replace=False)
+  ref = oracle.run_mh(spec, np.zeros((256, 10)), streams[:, :, pick])
+  assert np.array_equal(out['u'][pick], ref['u'])
+  assert _rel_err(out['v_x'][pick], ref['v_x'], 1.) <= RTOL
+  assert _rel_err(out['v_p'][pick], ref['v_p']) <= RTOL
