@@ -212,7 +212,8 @@ class SP:
       proposal = {'kind': 'gibbs', 'mean': targs[0], 'cov': targs[1],
                   'lo': [rv.vlims[0] for rv in rvs],
                   'hi': [rv.vlims[1] for rv in rvs],
-                  'tsteps': int(tkw.get('tsteps') or 1)}
+                  # rf.py:446-452: tsteps None/0 updates every coordinate
+                  'tsteps': int(tkw.get('tsteps') or d)}
       return make_spec(d, target, proposal, scores='gibbs', pscale=pscale,
                        prior=prior, ufun=ufun, names=names)
     proposal = self._lower_delta(rvs, names)
