@@ -53,14 +53,14 @@ def run_gibbs(spec, init, streams):
     cond_mod = 0
     xc = x[c]
     for t in range(T):
-      for key in range(cond_mod, min(cond_mod + tsteps, d)):
+      for j, key in enumerate(range(cond_mod, min(cond_mod + tsteps, d))):
         dmu = np.empty((d, 1), dtype=float)
         for i in range(d):
           if i != key:
             dmu[i] = xc[i] - mean[i]
         dmu = np.delete(dmu, (key), axis=0)
         lims = cdfs[key]
-        u = streams[t, 0, c]
+        u = streams[t, j, c]
         cdf = lims[0] + (lims[1] - lims[0]) * u     # legacy uniform(lo, hi)
         m = mean[key] + coef[key].dot(dmu).item()   # float(1x1 array)
         xc[key] = scipy.stats.norm.ppf(cdf, loc=m, scale=stdv[key])

@@ -18,10 +18,22 @@ import numpy as np
 
 
 def stream_width(spec):
-  """Draws per chain-step R."""
+  """Draws per chain-step R: d + 1 for MH, tsteps (one
+  uniform per updated coordinate, rf.py:446-458) for Gibbs."""
   if spec['proposal']['kind'] == 'gibbs':
-    return 1
+    return int(spec['proposal'].get('tsteps', 1))
   return int(spec['dim']) + 1
+
+
+def gibbs_coords(d, tsteps, n_steps):
+  """Coordinates per SP step under the per-RF cycling of rf.py:446-452."""
+  out, cm = [], 0
+  for _ in range(n_steps):
+    out.append(list(range(cm, min(cm + tsteps, d))))
+    cm += tsteps
+    if cm >= d:
+      cm = 0
+  return out
 
 
 def legacy_streams(spec, seeds, n_steps):
@@ -34,7 +46,9 @@ def legacy_streams(spec, seeds, n_steps):
     rs = np.random.RandomState(int(seed))
     col = out[:, :, c]
     if kind == 'gibbs':
-      col[:, 0] = rs.random_sample(n_steps)
+      col[:] = np.nan
+      for t, keys in enumerate(gibbs_coords(d, r, n_steps)):
+        col[t, :len(keys)] = rs.random_sample(len(keys))
       continue
     for t in range(n_steps):
       if kind == 'gauss':

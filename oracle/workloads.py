@@ -134,6 +134,14 @@ def spec_gibbs8(params):
                 ['x{}'.format(i) for i in range(8)])
 
 
+def spec_gibbs_sweep2(params):
+  """examples/cov/multinorm_rw.py model: CondCov tran without tsteps (every
+  coordinate per step)."""
+  sp = _gibbs([0.5, -0.5], [[1.5, -1.0], [-1.0, 2.]], -10., 10., ['x', 'y'])
+  sp['proposal']['tsteps'] = 2
+  return sp
+
+
 def spec_diag10(params):
   """SURVEY App. B H3 (cfg2 shape)."""
   d = len(params['mu'])
@@ -156,6 +164,7 @@ INITS = {
     'metrohast_norm1d': [50., 12.5], 'mcmc_prob2': [0.], 'mcmc_prob3': [5.],
     'mcmc_prob4a': [0., 1.], 'mcmc_prob4b': [5., 5.], 'mcmc_prob6': [0., 1.],
     'gibbs_norm2d': [0., 1.], 'diag10': [0.] * 10, 'gibbs8': [0.] * 8,
+    'gibbs_sweep2': [0., 0.],
     'gmm2': [0., 0.],
 }
 
@@ -165,6 +174,7 @@ WORKLOADS = {
     'mcmc_prob4b': spec_mcmc_prob4b, 'mcmc_prob6': spec_mcmc_prob6,
     'gibbs_norm2d': spec_gibbs_norm2d, 'diag10': spec_diag10,
     'gibbs8': spec_gibbs8, 'gmm2': spec_gmm2,
+    'gibbs_sweep2': spec_gibbs_sweep2,
 }
 
 

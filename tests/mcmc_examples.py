@@ -232,3 +232,22 @@ WORKLOADS = {
                   'sd': np.array([0.6, 0.8, 0.5]), 'step': 0.7},
            32, 256, 10000),
 }
+
+
+def gibbs_sweep2(pb, params):
+  """examples/cov/multinorm_rw.py:6-15 model (CondCov tran without tsteps:
+  every coordinate per step, rf.py:446-452) driven through SP with gibbs
+  scores."""
+  lims = (-10., 10.)
+  means = [0.5, -0.5]
+  covar = [[1.5, -1.0], [-1.0, 2.]]
+  x = pb.RV('x', vtype=float, vset=lims)
+  y = pb.RV('y', vtype=float, vset=lims)
+  process = pb.SP(x & y)
+  process.set_prob(scipy.stats.multivariate_normal, means, covar)
+  process.set_tran(scipy.stats.multivariate_normal, means, covar)
+  process.set_scores('gibbs')
+  return process, {'x': 0., 'y': 0.}, None, {}, ['x', 'y']
+
+
+WORKLOADS['gibbs_sweep2'] = (gibbs_sweep2, {}, 16, 256, 11000)
