@@ -52,6 +52,7 @@ struct pbh_engine {
   int64_t *nacc = nullptr;
   int64_t mom_steps = 0;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
+  bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
   // timing of the last pbh_run
   bool timed = false;
   int64_t last_launches = 0;
@@ -166,6 +167,7 @@ int pbh_create(int device, pbh_engine **out) {
   pbh_engine *e = new pbh_engine();
   e->device = device;
   if (const char *np = std::getenv("PBH_NO_PAIR")) e->pair_enabled = np[0] != '1';
+  if (const char *gm = std::getenv("PBH_GIBBS_MFMA")) e->gibbs_mfma = gm[0] != '0';
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -566,6 +568,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
                           ? v : (v <= k.log_npi ? std::exp(v) : 1.7976931348623158e+308);
     k.pair_ok = (e->pair_enabled && (k.scores == PBH_SCORES_METROPOLIS || qt > 0.0)) ? 1 : 0;
   }
+  k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384)
                          ? (size_t)k.tn * sizeof(double) : 0;

@@ -57,6 +57,7 @@ struct KArgs {
   int32_t debug;
   int64_t W;         // accept-mask words per recorded step = ceil(n / 64)
   int32_t pair_ok;   // engine allows the lane-pair kernel (see launch_mh_d)
+  int32_t gibbs_mfma;  // Gibbs density quadratic form on MFMA (d <= 16)
   // ---- moments ----
   double *msum, *msq;
   int64_t *nacc;

@@ -616,15 +616,78 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// MFMA form of the mvn quadratic form for a wavefront of 64 chains:
+//   Y^T (16 x 16 chains) = U^T (16 x 4) . DEV^T (4 x 16 chains), K-chunks of 4
+// with v_mfma_f64_16x16x4_f64 (A = U^T, constant, in VGPRs; B = the chains'
+// deviations, re-read from a per-wave LDS tile [chain][dim] so that lane l
+// holds chain l & 15's dim 4kc + (l >> 4)); then maha = sum_o y_o^2: four
+// squares per lane plus a two-step butterfly over the 16-lane groups leaves
+// every lane of group g holding its own chain's value -- no transposes back.
+// ---------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <int D>
+struct MvnMfma {
+  static constexpr int KC = (D + 3) / 4;     // K-chunks of 4 dims
+  static constexpr int S = KC * 4 + 1;       // LDS row stride (doubles), odd
+  double ua[KC];                              // A operand: U[4kc + l>>4][l&15]
+
+  __device__ __forceinline__ void init(const KArgs &a, double *tile) {
+    const int lane = threadIdx.x & 63;
+    const int o = lane & 15, k = lane >> 4;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int i = 4 * kc + k;
+      ua[kc] = (i < D && o < D) ? cld(a.tb, i * D + o) : 0.0;
+    }
+    double *row = tile + lane * S;
+#pragma unroll
+    for (int i = D; i < KC * 4; ++i) row[i] = 0.0;   // zero K padding
+  }
+
+  __device__ __forceinline__ double density(const KArgs &a, const double (&x)[D],
+                                            double *tile) const {
+    const int lane = threadIdx.x & 63;
+    double *row = tile + lane * S;
+#pragma unroll
+    for (int i = 0; i < D; ++i) row[i] = x[mvn_perm<D>(i)] - cld(a.ta, i);
+    double maha = 0.0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      const double *col = tile + (16 * g + (lane & 15)) * S + (lane >> 4);
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua[kc], col[4 * kc], acc, 0,
+                                                   0, 0);
+      double p = acc[0] * acc[0];
+      p = p + acc[1] * acc[1];
+      p = p + acc[2] * acc[2];
+      p = p + acc[3] * acc[3];
+      p = p + __shfl_xor(p, 16);
+      p = p + __shfl_xor(p, 32);
+      if ((lane >> 4) == g) maha = p;
+    }
+    const double logpdf = -0.5 * (cld(a.tc, 0) + maha);
+    return a.pscale == PBH_PSCALE_LIN ? exp(logpdf) : logpdf;
+  }
+};
+
+// ---------------------------------------------------------------------------
 // CondCov Gibbs kernel (cond_cov.py:42-65 per coordinate; rf.py:446-458
 // cycling).  One SP step updates tsteps coordinates; u is always True.
 // ---------------------------------------------------------------------------
-template <int D, int RNG>
+template <int D, int RNG, bool MF>
 __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
+  extern __shared__ double s_tile[];
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = c < a.n;
   const int64_t cc = active ? c : 0;
   const int lane = threadIdx.x & 63;
+  // MF: the density's quadratic form on the matrix cores (MvnMfma)
+  double *tile = s_tile + (threadIdx.x >> 6) * 64 * MvnMfma<D>::S;
+  MvnMfma<D> mf;
+  if (MF) mf.init(a, tile);
   double x[D], ms[D], mq[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
@@ -669,7 +732,7 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
         x[k] = ndtri(cdf) * cld(a.gstdv, k) + m;        // norm.ppf(cdf, m, sd)
       }
     }
-    lp = mvn_density<D>(a, x);
+    lp = MF ? mf.density(a, x, tile) : mvn_density<D>(a, x);
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       ms[k] += x[k];
@@ -776,10 +839,24 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
 template <int D>
 hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
   const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
+  if constexpr (D <= 16) {
+    if (a.gibbs_mfma) {
+      const size_t lds = (kBlock / 64) * 64 * MvnMfma<D>::S * sizeof(double);
+      if (a.rng == PBH_RNG_REPLAY)
+        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, true>), grid, block,
+                           lds, st, a);
+      else
+        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, true>), grid, block,
+                           lds, st, a);
+      return hipGetLastError();
+    }
+  }
   if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, false>), grid, block, 0,
+                       st, a);
   else
-    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, false>), grid, block, 0,
+                       st, a);
   return hipGetLastError();
 }
 

@@ -244,3 +244,20 @@ def test_full_size_cfg2_replay_parity():
   assert np.array_equal(out['u'][pick], ref['u'])
   assert _rel_err(out['v_x'][pick], ref['v_x'], 1.) <= RTOL
   assert _rel_err(out['v_p'][pick], ref['v_p']) <= RTOL
+
+
+@pytest.mark.parametrize('name', ['gibbs8', 'gibbs_norm2d', 'gibbs_sweep2'])
+def test_gibbs_density_mfma_matches_valu(name, monkeypatch):
+  """The Gibbs v.prob quadratic form on MFMA (v_mfma_f64_16x16x4_f64) and on
+  the VALU agree to fp64 rounding and both match the reference."""
+  g = oracle.load_golden(name)
+  spec = oracle.golden_spec(name, g)
+  n, t = g['v_x'].shape[:2]
+  streams = oracle.legacy_streams(spec, g['seeds'], t)
+  outs = {}
+  for mf in ('1', '0'):
+    monkeypatch.setenv('PBH_GIBBS_MFMA', mf)
+    outs[mf], _ = _run_replay(spec, golden_init(name, n), streams, debug=False)
+  assert np.array_equal(outs['1']['v_x'], outs['0']['v_x'])
+  assert _rel_err(outs['1']['v_p'], outs['0']['v_p']) <= 1e-13
+  assert _rel_err(outs['1']['v_p'], g['v_p']) <= RTOL
