@@ -256,6 +256,16 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
     }
     ow = pack(blk, w.data(), d);
   }
+  if (m->target_kind == PBH_TARGET_NORM_IID) {
+    // Production path: centred sufficient statistics of the observations,
+    // sum_j (obs_j - mu)^2 = S2 + n (obar - mu)^2 -> O(1) per chain-step.
+    double mean = 0., s2 = 0.;
+    for (int64_t j = 0; j < m->n; ++j) mean += A[j];
+    mean /= (double)m->n;
+    for (int64_t j = 0; j < m->n; ++j) s2 += (A[j] - mean) * (A[j] - mean);
+    const double st[2] = {mean, s2};
+    ow = pack(blk, st, 2);
+  }
   uint32_t lo_incl = 0, hi_incl = 0, ufun = 0;
   if (m->has_prior) {
     if (!m->prior_lo || !m->prior_hi || !m->prior_lo_incl || !m->prior_hi_incl)
@@ -570,7 +580,8 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   }
   k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
-  const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384)
+  const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
+                      k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
                          ? (size_t)k.tn * sizeof(double) : 0;
   HIP_TRY(hipEventRecord(e->ev0, e->stream));
   int64_t launches = 0;

@@ -125,7 +125,13 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
       }
       const double lsg = log(sg);
       const double logC = a.norm_logC;
-      if (use_lds) {
+      if (FAST) {
+        // production path: sufficient statistics (obar, S2) of the data
+        const double n = (double)a.tn;
+        const double dm = cld(a.tw, 0) - mu;
+        const double ss = __builtin_fma(n * dm, dm, cld(a.tw, 1));
+        out = -0.5 * ss / (sg * sg) - n * (logC + lsg);
+      } else if (use_lds) {
         out = np_pairwise(
             [&](int64_t j) { return norm_logpdf(obs_lds[j], mu, sg, lsg, logC); },
             a.tn);
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   const int lane = threadIdx.x & 63;
 
   bool use_lds = false;
-  if ((TGT == 0 || TGT == PBH_TARGET_NORM_IID) &&
+  if (!FAST && (TGT == 0 || TGT == PBH_TARGET_NORM_IID) &&
       a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
     for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = cld(a.ta, j);
     __syncthreads();
