@@ -261,3 +261,22 @@ def test_gibbs_density_mfma_matches_valu(name, monkeypatch):
   assert np.array_equal(outs['1']['v_x'], outs['0']['v_x'])
   assert _rel_err(outs['1']['v_p'], outs['0']['v_p']) <= 1e-13
   assert _rel_err(outs['1']['v_p'], g['v_p']) <= RTOL
+
+
+@pytest.mark.parametrize('n_obs', [7, 129, 1000, 20000])
+def test_iid_normal_pairwise_tree_matches_numpy(n_obs):
+  """PD.prod's np.sum over observations (pd.py:368) is reproduced by the
+  kernel's numpy pairwise tree: leaf < 8, 8-accumulator leaves, the split
+  recursion beyond 128 terms, and the global-memory path beyond the LDS
+  stage (> 16 384 observations)."""
+  g = oracle.load_golden('metrohast_norm1d')
+  spec = oracle.golden_spec('metrohast_norm1d', g)
+  spec['target']['obs'] = np.random.RandomState(n_obs).normal(50., 10., n_obs)
+  n, t = 64, 40
+  streams = oracle.legacy_streams(spec, np.arange(n) + 123, t)
+  init = golden_init('metrohast_norm1d', n)
+  out, _ = _run_replay(spec, init, streams, debug=True)
+  ref = oracle.run_mh(spec, init, streams)
+  assert np.array_equal(out['u'], ref['u'])
+  assert _rel_err(out['p_p'], ref['p_p']) <= RTOL
+  assert _rel_err(out['v_x'], ref['v_x'], 1.) <= RTOL
