@@ -89,17 +89,15 @@ def test_example_scripts_reproduce_reference_chains(name):
     assert _golden_rtol(np.asarray(summary.v.prob), g['v_p'][c]) <= 1e-12
     assert summary.u.count(True) == int(g['u'][c].sum())
     # the global legacy stream advanced exactly as the reference's did
-    rs = np.random.RandomState(int(g['seeds'][c]))
-    oracle.legacy_streams  # (documentation: same consumption order)
-    d = len(keys)
-    for _ in range(t):
-      if name.startswith('gibbs'):
-        rs.random_sample()
-      elif name == 'metrohast_norm1d':
-        rs.random_sample(d); rs.random_sample()
-      else:
-        rs.standard_normal(d); rs.random_sample()
-    assert np.random.random_sample() == rs.random_sample()
+    spec = oracle.golden_spec(name, g)
+    ref_stream = oracle.legacy_streams(spec, g['seeds'][c:c + 1], t + 1)
+    nxt = ref_stream[t, 0, 0]
+    if spec['proposal']['kind'] == 'gauss':   # next draw would be a gauss
+      rs = np.random.RandomState(int(g['seeds'][c]))
+      for _ in range(t):
+        rs.standard_normal(len(keys)); rs.random_sample()
+      nxt = rs.random_sample()
+    assert np.random.random_sample() == nxt
 
 
 @pytest.mark.gpu
