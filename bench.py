@@ -118,7 +118,9 @@ def main():
   spec = cfg2_spec()
   n = args.chains
   eng = Engine(spec, device=local)
-  eng.init_chains(np.zeros((n, D)), chain_offset=rank * n)
+  from probayes_amd.dist import shard
+  offset, n = shard(n * world, rank, world)   # weak scaling: n chains / GPU
+  eng.init_chains(np.zeros((n, D)), chain_offset=offset)
   eng.set_rng(args.rng, seed=20261015)
   if not args.no_trace:
     eng.alloc_trace(args.warmup + args.steps, 1)
@@ -183,7 +185,7 @@ def main():
                                 else measured_traffic(n, spl, args.rng,
                                                       not args.no_trace),
                      'bytes_per_chain_step': bpcs,
-                     'kernel': 'mh_kernel<10, PHILOX>',
+                     'kernel': 'mh_pair_kernel<10, PHILOX>' if not os.environ.get('PBH_NO_PAIR') else 'mh_kernel<10, PHILOX, DIAG, GAUSS>',
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),

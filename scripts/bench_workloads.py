@@ -46,6 +46,7 @@ def run(name, n, steps, rng='philox', spl=0, trace=True):
   init = oracle.workloads.golden_init(name, n)
   eng.init_chains(init)
   eng.set_rng(rng, seed=11)
+  eng.run(8)          # warm-up launch (code-object load stays untimed)
   if trace:
     eng.alloc_trace(steps, 1)
   eng.run(steps, steps_per_launch=spl)
