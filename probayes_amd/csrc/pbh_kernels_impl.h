@@ -293,6 +293,11 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
 
+  // record phase / index of the trace, advanced per step (no 64-bit
+  // division in the loop): step g records iff (g + 1) % thin == 0, at
+  // record (g + 1) / thin - 1 - rec_base.
+  int ph = (int)((a.g0 + 1) % a.thin);
+  int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     // ---- draws ----
@@ -403,8 +408,11 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       mq[k] += x[k] * x[k];
     }
     // ---- trace (every thin-th step, wave-uniform condition) ----
-    if ((g + 1) % a.thin == 0) {
-      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+    const bool rec_now = ph == 0;
+    const int64_t rec = ri;
+    ph = (ph + 1 == a.thin) ? 0 : ph + 1;   // next step's phase
+    ri += (ph == 0) ? 1 : 0;
+    if (rec_now) {
       if (rec >= 0 && rec < a.rec_cap) {
         if (active) {
 #pragma unroll
@@ -485,6 +493,11 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
 
+  // record phase / index of the trace, advanced per step (no 64-bit
+  // division in the loop): step g records iff (g + 1) % thin == 0, at
+  // record (g + 1) / thin - 1 - rec_base.
+  int ph = (int)((a.g0 + 1) % a.thin);
+  int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     double r[H];
@@ -591,8 +604,11 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       ms[i] += x[i];
       mq[i] += x[i] * x[i];
     }
-    if ((g + 1) % a.thin == 0) {
-      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+    const bool rec_now = ph == 0;
+    const int64_t rec = ri;
+    ph = (ph + 1 == a.thin) ? 0 : ph + 1;   // next step's phase
+    ri += (ph == 0) ? 1 : 0;
+    if (rec_now) {
       if (rec >= 0 && rec < a.rec_cap) {
         if (active) {
 #pragma unroll
@@ -706,6 +722,11 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
   const int ts = a.tsteps;
   const int nblk = (D + ts - 1) / ts;
 
+  // record phase / index of the trace, advanced per step (no 64-bit
+  // division in the loop): step g records iff (g + 1) % thin == 0, at
+  // record (g + 1) / thin - 1 - rec_base.
+  int ph = (int)((a.g0 + 1) % a.thin);
+  int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     const int cm = (int)(g % nblk) * ts;
@@ -744,8 +765,11 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
       ms[k] += x[k];
       mq[k] += x[k] * x[k];
     }
-    if ((g + 1) % a.thin == 0) {
-      const int64_t rec = (g + 1) / a.thin - 1 - a.rec_base;
+    const bool rec_now = ph == 0;
+    const int64_t rec = ri;
+    ph = (ph + 1 == a.thin) ? 0 : ph + 1;   // next step's phase
+    ri += (ph == 0) ? 1 : 0;
+    if (rec_now) {
       if (rec >= 0 && rec < a.rec_cap) {
         if (active) {
 #pragma unroll
