@@ -26,14 +26,6 @@ constexpr double kNearlyNegInf = -1.7976931348623158e+308;
 // ---------------------------------------------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 
-// a ^ b ^ k with k wave-uniform: one v_xor3_b32 (hipcc does not form it on
-// gfx950 by itself; the Philox round needs two per round).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
-  uint32_t r;
-  asm("v_xor3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-  return r;
-}
-
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
                                                 uint32_t k1) {
   constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
@@ -44,7 +36,7 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
     const uint64_t p1 = (uint64_t)M1 * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = u32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += W0;
     k1 += W1;
   }
