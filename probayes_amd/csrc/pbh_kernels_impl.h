@@ -289,7 +289,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     mq[k] = 0.;
   }
   double lp = a.lp[cc];
-  double eB = lin ? lp : exp_logp(lp, a.log_npi);
+  double eB = lin ? lp : (FAST ? exp_logp_fast(lp, a.log_npi)
+                              : exp_logp(lp, a.log_npi));
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
 
@@ -387,7 +388,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     }
     // ---- density, score, accept ----
     const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
-    const double eA = lin ? lpp : exp_logp(lpp, a.log_npi);
+    const double eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
+                                        : exp_logp(lpp, a.log_npi));
     double sc = __builtin_nan("");
     bool acc;
     if (!a.has_pred && s == 0) {
@@ -489,7 +491,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     mq[i] = 0.;
   }
   double lp = a.lp[cc];
-  double eB = lin ? lp : exp_logp(lp, a.log_npi);
+  double eB = lin ? lp : (FAST ? exp_logp_fast(lp, a.log_npi)
+                              : exp_logp(lp, a.log_npi));
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
 
@@ -577,7 +580,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     uint32_t acc_bit = 0;
     double eA = 0.;
     if (hi) {
-      eA = lin ? lpp : exp_logp(lpp, a.log_npi);
+      eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
+                             : exp_logp(lpp, a.log_npi));
       bool acc;
       if (!a.has_pred && s == 0) {
         acc = true;

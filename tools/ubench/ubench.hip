@@ -56,6 +56,11 @@ __global__ void k_exp64(double *out, double s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+__global__ void k_expcheck(double *out, const double *x, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { out[2 * i] = exp(x[i]); out[2 * i + 1] = fast_exp(x[i]); }
+}
+
 template <class K, class T>
 float timeit(K k, T *buf, T s, int blocks) {
   hipEvent_t e0, e1;
@@ -87,5 +92,20 @@ int main() {
   printf("philox    %8.3f ms  %.1f ns per call per wave-slot\n", pm, pm * 1e6 / (waves * R / 16) * simds);
   float em = timeit(k_exp64, d, 0.5, blocks);
   printf("exp_f64   %8.3f ms  %.1f ns per call per wave-slot\n", em, em * 1e6 / (waves * R / 16) * simds);
+  // fast_exp accuracy against ocml exp over [-746, 710]
+  const int n = 1 << 20;
+  double *hx = new double[n], *ho = new double[2 * n], *dx, *dout;
+  for (int i = 0; i < n; ++i) hx[i] = -746.0 + 1456.0 * (i + 0.5) / n;
+  hipMalloc(&dx, n * 8); hipMalloc(&dout, 2 * n * 8);
+  hipMemcpy(dx, hx, n * 8, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_expcheck, dim3(n / 256), dim3(256), 0, 0, dout, dx, n);
+  hipMemcpy(ho, dout, 2 * n * 8, hipMemcpyDeviceToHost);
+  long long maxulp = 0;
+  for (int i = 0; i < n; ++i) {
+    long long a = *(long long *)&ho[2 * i], b = *(long long *)&ho[2 * i + 1];
+    long long dd = a > b ? a - b : b - a;
+    if (ho[2 * i] > 2.3e-308 && dd > maxulp) maxulp = dd;
+  }
+  printf("fast_exp max ulp vs ocml exp (normal range): %lld\n", maxulp);
   return 0;
 }
