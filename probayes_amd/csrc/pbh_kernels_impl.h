@@ -501,6 +501,36 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   // record (g + 1) / thin - 1 - rec_base.
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+
+  // production draws of one step for this half: ceil(H/2) normal pairs, two
+  // pairs per Philox block; an odd pair count leaves the last block's second
+  // half for the 53-bit threshold (used by the upper half)
+  auto draw_fast = [&](int64_t gg, double (&rr)[H], double &tt) {
+    constexpr int P = (H + 1) / 2;
+#pragma unroll
+    for (int q = 0; q < (P + 1) / 2; ++q) {
+      const u32x4 w = philox4x32_10(ctr(q + 16 * h, gg, chain), a.seed_lo, a.seed_hi);
+      double z1;
+      const double z0 = fast_normal_pair(w.x, w.z, z1);
+      if (4 * q < H) rr[4 * q] = z0;
+      if (4 * q + 1 < H) rr[4 * q + 1] = z1;
+      if (2 * q + 1 < P) {
+        double z3;
+        const double z2 = fast_normal_pair(w.y, w.w, z3);
+        if (4 * q + 2 < H) rr[4 * q + 2] = z2;
+        if (4 * q + 3 < H) rr[4 * q + 3] = z3;
+      } else {
+        tt = u01(w.y, w.w);
+      }
+    }
+    if (P % 2 == 0) {
+      const u32x4 w = philox4x32_10(ctr(0xFFFFu, gg, chain), a.seed_lo, a.seed_hi);
+      tt = u01(w.x, w.y);
+    }
+  };
+  double rn[H], thrn = 0.;
+  if (FAST) draw_fast(a.g0, rn, thrn);
+
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     double r[H];
@@ -511,28 +541,13 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
       if (hi) thr = row[(int64_t)D * a.n];
     } else if (FAST) {
-      // per half: ceil(H/2) normal pairs, two pairs per Philox block
-      constexpr int P = (H + 1) / 2;
+      // software-pipelined: this step's draws were generated last iteration
+      // (they do not depend on the chain state); issue the next step's
+      // Philox blocks now so they overlap this step's fp64 chain.
 #pragma unroll
-      for (int q = 0; q < (P + 1) / 2; ++q) {
-        const u32x4 w = philox4x32_10(ctr(q + 16 * h, g, chain), a.seed_lo, a.seed_hi);
-        double z1;
-        const double z0 = fast_normal_pair(w.x, w.z, z1);
-        if (4 * q < H) r[4 * q] = z0;
-        if (4 * q + 1 < H) r[4 * q + 1] = z1;
-        if (2 * q + 1 < P) {
-          double z3;
-          const double z2 = fast_normal_pair(w.y, w.w, z3);
-          if (4 * q + 2 < H) r[4 * q + 2] = z2;
-          if (4 * q + 3 < H) r[4 * q + 3] = z3;
-        } else {
-          thr = u01(w.y, w.w);   // spare half-block (used by half 1)
-        }
-      }
-      if (P % 2 == 0 && hi) {
-        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
-        thr = u01(w.x, w.y);
-      }
+      for (int i = 0; i < H; ++i) r[i] = rn[i];
+      thr = thrn;
+      draw_fast(g + 1, rn, thrn);
     } else {
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
@@ -576,32 +591,20 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 #pragma unroll
       for (int i = 0; i < H; ++i) lpp = lpp + r[i];
     }
-    // only half 1's lpp is the full density; score there
-    uint32_t acc_bit = 0;
-    double eA = 0.;
-    if (hi) {
-      eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
-                             : exp_logp(lpp, a.log_npi));
-      bool acc;
-      if (!a.has_pred && s == 0) {
-        acc = true;
-      } else {
-        double q = eA / np_max_tiny(eB);
-        q = q < 1. ? q : 1.;
-        acc = q >= thr;
-      }
-      acc_bit = acc ? 1u : 0u;
-    }
+    // half 1 holds the full density and the threshold: its decision is the
+    // chain's (computed branch-free in both halves; half 0's is discarded)
+    const double eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
+                                        : exp_logp(lpp, a.log_npi));
+    double q = eA / np_max_tiny(eB);
+    q = q < 1. ? q : 1.;
+    const bool first = !a.has_pred && s == 0;   // s = None on step 1
+    const uint32_t acc_bit = (first || q >= thr) ? 1u : 0u;
     const uint32_t acc_lo = swap_u32(acc_bit, hi);   // half 0 receives it
     const bool acc = (hi ? acc_bit : acc_lo) != 0;
-    if (acc) {
 #pragma unroll
-      for (int i = 0; i < H; ++i) x[i] = xp[i];
-      if (hi) {
-        lp = lpp;
-        eB = eA;
-      }
-    }
+    for (int i = 0; i < H; ++i) x[i] = acc ? xp[i] : x[i];
+    lp = (acc && hi) ? lpp : lp;
+    eB = (acc && hi) ? eA : eB;
     nacc += acc ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < H; ++i) {
@@ -731,6 +734,7 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
   // record (g + 1) / thin - 1 - rec_base.
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     const int cm = (int)(g % nblk) * ts;
