@@ -102,7 +102,8 @@ def main():
   ap.add_argument('--chains', type=int, default=65536, help='per GPU')
   ap.add_argument('--steps-per-launch', type=int, default=250)
   ap.add_argument('--no-trace', action='store_true')
-  ap.add_argument('--rng', default='philox', choices=['philox', 'philox_f64'])
+  ap.add_argument('--rng', default='philox',
+                  choices=['philox', 'philox_f64', 'xoshiro'])
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--traffic-bytes', type=float, default=None,
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
@@ -173,9 +174,12 @@ def main():
                                'MH, {} chains/GPU, full trace every step'
                                .format(n),
                    'chains_per_gpu': n, 'dim': D,
-                   'rng': 'philox4x32-10 ({})'.format(
-                       'fp32 Box-Muller normals, exact sign symmetry'
-                       if args.rng == 'philox' else 'fp64 Box-Muller normals'),
+                   'rng': {'philox': 'philox4x32-10, fp32 Box-Muller normals '
+                                     'with exact sign symmetry',
+                           'philox_f64': 'philox4x32-10, fp64 Box-Muller normals',
+                           'xoshiro': 'xoshiro128** per chain, fp32 Box-Muller '
+                                      'normals with exact sign symmetry'
+                           }[args.rng],
                    'trace': not args.no_trace, 'steps_per_launch': spl,
                    'parallelism': 'chain-sharded x{}'.format(world)},
         'roofline': {'bound': 'hbm', 'achieved': achieved,

@@ -63,8 +63,11 @@ enum pbh_rng_mode {
   PBH_RNG_PHILOX = 1,    /* production: Philox-4x32-10 keyed by (seed, global
                             chain id); fp32 Box-Muller normals with exact sign
                             symmetry, FMA-corrected divisions                 */
-  PBH_RNG_PHILOX_F64 = 2 /* Philox-4x32-10 with fp64 Box-Muller normals and
+  PBH_RNG_PHILOX_F64 = 2, /* Philox-4x32-10 with fp64 Box-Muller normals and
                             the reference arithmetic of REPLAY                 */
+  PBH_RNG_XOSHIRO = 3    /* production, fastest: one xoshiro128** stream per
+                            chain (per lane half), seeded by SplitMix64 of
+                            (seed, global chain id); otherwise as PHILOX      */
 };
 
 /* Joint density + acceptance (replaces RF.set_prob/set_tran + SP.set_scores:

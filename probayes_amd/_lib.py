@@ -21,7 +21,7 @@ PSCALE = {'log': 0, 'lin': 1}
 SCORES = {'hastings': 1, 'metropolis': 2, 'gibbs': 3}
 TRAN = {'const': 1, 'gauss_pdf': 2}
 PROPOSAL = {'gauss': 1, 'sphere': 2, 'uniform': 3, 'gibbs': 4}
-RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2}
+RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2, 'xoshiro': 3}
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)

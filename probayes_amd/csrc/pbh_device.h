@@ -43,6 +43,35 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
   return c;
 }
 
+// xoshiro128** (Blackman & Vigna 2018): 128-bit state, 32-bit outputs,
+// passes BigCrush; ~10 full-rate integer ops per word against ~55 mixed-rate
+// ops per 4 words of Philox-4x32-10 (20 of them v_mad_u64_u32).  One
+// independent stream per chain (per lane half), seeded by SplitMix64.
+struct Xo { uint32_t s0, s1, s2, s3; };
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) {
+  return (x << k) | (x >> (32 - k));
+}
+
+__device__ __forceinline__ uint32_t xo_next(Xo &s) {
+  const uint32_t r = rotl32(s.s1 * 5u, 7) * 9u;
+  const uint32_t t = s.s1 << 9;
+  s.s2 ^= s.s0;
+  s.s3 ^= s.s1;
+  s.s1 ^= s.s2;
+  s.s0 ^= s.s3;
+  s.s2 ^= t;
+  s.s3 = rotl32(s.s3, 11);
+  return r;
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t &z) {
+  uint64_t x = (z += 0x9E3779B97F4A7C15ull);
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
 // 53-bit double in [0, 1) from two words, the same construction as NumPy's
 // legacy random_sample: ((a >> 5) * 2^26 + (b >> 6)) / 2^53.
 __device__ __forceinline__ double u01(uint32_t a, uint32_t b) {

@@ -40,6 +40,8 @@ struct pbh_engine {
   uint64_t seed = 0;
   double *rep = nullptr;
   int64_t rep_steps = 0, rep_g0 = 0;
+  uint32_t *xo = nullptr;      // xoshiro128** states [4][2][n]
+  bool xo_seeded = false;
   // trace
   int64_t cap = 0;
   int32_t thin = 1, debug = 0;
@@ -186,7 +188,7 @@ int pbh_destroy(pbh_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
-  dfree(e->x); dfree(e->lp); dfree(e->rep);
+  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo);
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
@@ -423,6 +425,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
     if (!rc) rc = dalloc(e->msum, (size_t)n * d);
     if (!rc) rc = dalloc(e->msq, (size_t)n * d);
     if (!rc) rc = dalloc(e->nacc, n);
+    if (!rc) rc = dalloc(e->xo, (size_t)8 * n);
     if (rc) return rc;
   }
   std::vector<double> xt((size_t)n * d);
@@ -435,6 +438,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   HIP_TRY(hipMemset(e->nacc, 0, n * sizeof(int64_t)));
   e->n = n;
   e->off = off;
+  e->xo_seeded = false;
   e->has_pred = false;
   e->g = 0;
   e->mom_steps = 0;
@@ -448,10 +452,11 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
 int pbh_set_rng(pbh_engine *e, int32_t mode, uint64_t seed) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX &&
-      mode != PBH_RNG_PHILOX_F64)
+      mode != PBH_RNG_PHILOX_F64 && mode != PBH_RNG_XOSHIRO)
     return fail(PBH_ERR_ARG, "bad rng mode %d", mode);
   e->rng = mode;
   e->seed = seed;
+  e->xo_seeded = false;   // (re)seeded from (seed, chain id) at the next run
   return PBH_OK;
 }
 
@@ -552,6 +557,10 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
                   (long long)e->cap, (long long)recs);
   }
   HIP_TRY(hipSetDevice(e->device));
+  if (e->rng == PBH_RNG_XOSHIRO && !e->xo_seeded) {
+    HIP_TRY(pbh::launch_xo_seed(e->xo, e->n, e->off, e->seed, e->stream));
+    e->xo_seeded = true;
+  }
   const int64_t spl = steps_per_launch > 0 ? steps_per_launch : n_steps;
   KArgs k = e->k;
   k.n = e->n;
@@ -562,6 +571,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.seed_lo = (uint32_t)e->seed;
   k.seed_hi = (uint32_t)(e->seed >> 32);
   k.rep = e->rep;
+  k.xo = e->xo;
   k.tx = e->tx; k.tlp = e->tlp; k.tpx = e->tpx; k.tpp = e->tpp; k.ts = e->ts;
   k.tacc = e->tacc;
   k.thin = e->cap > 0 ? e->thin : 1;

@@ -46,6 +46,7 @@ struct KArgs {
   int32_t rng;       // PBH_RNG_*
   uint32_t seed_lo, seed_hi;
   const double *rep; // replay stream [T][R][n]
+  uint32_t *xo;      // xoshiro128** states [4][2][n] (word, lane half, chain)
   int64_t rep_row0;  // replay step index of g0
   int32_t R;         // replay draws per step
   // ---- trace ----
@@ -66,6 +67,8 @@ struct KArgs {
 // Host launchers (pbh_kernels.hip).
 hipError_t launch_mh(const KArgs &a, hipStream_t s, size_t lds_bytes);
 hipError_t launch_gibbs(const KArgs &a, hipStream_t s);
+hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
+                          hipStream_t s);
 bool mh_dim_supported(int d);
 
 }  // namespace pbh

@@ -62,6 +62,19 @@ __device__ __forceinline__ double uniform_pdf(double x, double lo,
   return (0.0 <= y && y <= 1.0) ? 1.0 / scale : 0.0;
 }
 
+__device__ __forceinline__ Xo xo_load(const KArgs &a, int h, int64_t c) {
+  return Xo{a.xo[(0 * 2 + h) * a.n + c], a.xo[(1 * 2 + h) * a.n + c],
+            a.xo[(2 * 2 + h) * a.n + c], a.xo[(3 * 2 + h) * a.n + c]};
+}
+
+__device__ __forceinline__ void xo_store(const KArgs &a, int h, int64_t c,
+                                         const Xo &s) {
+  a.xo[(0 * 2 + h) * a.n + c] = s.s0;
+  a.xo[(1 * 2 + h) * a.n + c] = s.s1;
+  a.xo[(2 * 2 + h) * a.n + c] = s.s2;
+  a.xo[(3 * 2 + h) * a.n + c] = s.s3;
+}
+
 __device__ __forceinline__ u32x4 ctr(uint32_t j, int64_t g, int64_t chain) {
   return u32x4{j, (uint32_t)g, (uint32_t)chain,
                (uint32_t)((uint64_t)chain >> 32) ^
@@ -264,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   // 0 keeps the wave-uniform runtime switch (any model, one binary).
   // FAST = production Philox path (fp32 normals, FMA-corrected divisions);
   // REPLAY and PHILOX_F64 keep the reference's arithmetic exactly.
-  constexpr bool FAST = RNG == PBH_RNG_PHILOX;
+  constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   const int prop = PROP ? PROP : a.prop;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   extern __shared__ double s_obs[];
@@ -293,6 +306,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
                               : exp_logp(lp, a.log_npi));
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
+  Xo xs{0u, 0u, 0u, 0u};
+  if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, 0, cc);
 
   // record phase / index of the trace, advanced per step (no 64-bit
   // division in the loop): step g records iff (g + 1) % thin == 0, at
@@ -309,6 +324,26 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 #pragma unroll
       for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
       thr = row[(int64_t)D * a.n];
+    } else if (RNG == PBH_RNG_XOSHIRO) {
+      // two words per normal pair / per 53-bit uniform, in draw order
+      if (prop == PBH_PROP_GAUSS) {
+#pragma unroll
+        for (int p = 0; p < (D + 1) / 2; ++p) {
+          const uint32_t wu = xo_next(xs);
+          const uint32_t wa = xo_next(xs);
+          double z1;
+          r[2 * p] = fast_normal_pair(wu, wa, z1);
+          if (2 * p + 1 < D) r[2 * p + 1] = z1;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const uint32_t w0 = xo_next(xs);
+          r[k] = u01(w0, xo_next(xs));
+        }
+      }
+      const uint32_t t0 = xo_next(xs);
+      thr = u01(t0, xo_next(xs));
     } else if (FAST && prop == PBH_PROP_GAUSS) {
       // two normal pairs per Philox block; an odd pair count leaves the
       // block's second half for the 53-bit threshold
@@ -443,6 +478,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     }
     a.lp[c] = lp;
     a.nacc[c] += nacc;
+    if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
   }
 }
 
@@ -472,7 +508,7 @@ template <int D, int RNG>
 __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
   constexpr int H = D / 2;
-  constexpr bool FAST = RNG == PBH_RNG_PHILOX;
+  constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   const int lane = threadIdx.x & 63;
   const bool hi = lane >= 32;
@@ -495,6 +531,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
                               : exp_logp(lp, a.log_npi));
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
+  Xo xs{0u, 0u, 0u, 0u};
+  if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, h, cc);
 
   // record phase / index of the trace, advanced per step (no 64-bit
   // division in the loop): step g records iff (g + 1) % thin == 0, at
@@ -529,7 +567,7 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     }
   };
   double rn[H], thrn = 0.;
-  if (FAST) draw_fast(a.g0, rn, thrn);
+  if (RNG == PBH_RNG_PHILOX) draw_fast(a.g0, rn, thrn);
 
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
@@ -540,6 +578,19 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 #pragma unroll
       for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
       if (hi) thr = row[(int64_t)D * a.n];
+    } else if (RNG == PBH_RNG_XOSHIRO) {
+      // this half's stream: two words per normal pair, then the threshold
+      // (drawn by both halves so each stream advances the same per step)
+#pragma unroll
+      for (int p = 0; p < (H + 1) / 2; ++p) {
+        const uint32_t wu = xo_next(xs);
+        const uint32_t wa = xo_next(xs);
+        double z1;
+        r[2 * p] = fast_normal_pair(wu, wa, z1);
+        if (2 * p + 1 < H) r[2 * p + 1] = z1;
+      }
+      const uint32_t t0 = xo_next(xs);
+      thr = u01(t0, xo_next(xs));
     } else if (FAST) {
       // software-pipelined: this step's draws were generated last iteration
       // (they do not depend on the chain state); issue the next step's
@@ -641,6 +692,7 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       a.lp[c] = lp;
       a.nacc[c] += nacc;
     }
+    if (RNG == PBH_RNG_XOSHIRO) xo_store(a, h, c, xs);
   }
 }
 
@@ -726,6 +778,8 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
   }
   double lp = a.lp[cc];
   const int64_t chain = a.off + cc;
+  Xo xs{0u, 0u, 0u, 0u};
+  if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, 0, cc);
   const int ts = a.tsteps;
   const int nblk = (D + ts - 1) / ts;
 
@@ -745,6 +799,9 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
         double u;
         if (RNG == PBH_RNG_REPLAY) {
           u = a.rep[((a.rep_row0 + s) * a.R + j) * a.n + cc];
+        } else if (RNG == PBH_RNG_XOSHIRO) {
+          const uint32_t w0 = xo_next(xs);
+          u = u01(w0, xo_next(xs));
         } else {
           const u32x4 w = philox4x32_10(ctr(j, g, chain), a.seed_lo, a.seed_hi);
           u = u01(w.x, w.y);
@@ -805,6 +862,7 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
     }
     a.lp[c] = lp;
     a.nacc[c] += a.n_steps;
+    if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
   }
 }
 
@@ -819,6 +877,9 @@ void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
   else if (a.rng == PBH_RNG_PHILOX)
     hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX, TGT, PROP>), grid, block,
                        lds, st, a);
+  else if (a.rng == PBH_RNG_XOSHIRO)
+    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_XOSHIRO, TGT, PROP>), grid, block,
+                       lds, st, a);
   else
     hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX_F64, TGT, PROP>), grid,
                        block, lds, st, a);
@@ -832,6 +893,8 @@ void launch_mh_pair(const KArgs &a, hipStream_t st) {
     hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_REPLAY>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_PHILOX)
     hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_XOSHIRO)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_XOSHIRO>), grid, block, 0, st, a);
   else
     hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_F64>), grid, block, 0, st, a);
 }
@@ -883,6 +946,9 @@ hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
       if (a.rng == PBH_RNG_REPLAY)
         hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, true>), grid, block,
                            lds, st, a);
+      else if (a.rng == PBH_RNG_XOSHIRO)
+        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_XOSHIRO, true>), grid, block,
+                           lds, st, a);
       else
         hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, true>), grid, block,
                            lds, st, a);
@@ -891,6 +957,9 @@ hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
   }
   if (a.rng == PBH_RNG_REPLAY)
     hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, false>), grid, block, 0,
+                       st, a);
+  else if (a.rng == PBH_RNG_XOSHIRO)
+    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_XOSHIRO, false>), grid, block, 0,
                        st, a);
   else
     hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, false>), grid, block, 0,

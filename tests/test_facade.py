@@ -116,10 +116,11 @@ def test_batched_sampler_reproduces_all_reference_chains(name):
 
 
 @pytest.mark.gpu
-def test_batched_philox_sampler_posterior():
+@pytest.mark.parametrize('rng', ['philox', 'xoshiro'])
+def test_batched_philox_sampler_posterior(rng):
   """metrohast_norm1d posterior with 4096 production chains."""
   process, init, extra, kwds, keys, g = _build('metrohast_norm1d')
-  sampler = process.sampler(init, extra, stop=2000, chains=4096, rng='philox',
+  sampler = process.sampler(init, extra, stop=2000, chains=4096, rng=rng,
                             seed=7, **kwds)
   summary = process(process.walk(sampler))
   mus = np.asarray(summary.v['mu'])[500:]

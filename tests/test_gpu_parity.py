@@ -99,7 +99,7 @@ def _diag10_spec():
   return oracle.golden_spec('diag10')
 
 
-@pytest.mark.parametrize('mode', ['philox', 'philox_f64'])
+@pytest.mark.parametrize('mode', ['philox', 'philox_f64', 'xoshiro'])
 def test_philox_diag10_statistics_and_invariants(mode):
   """cfg2 model in production (Philox) mode: the posterior matches the
   target within Monte-Carlo error; traces are deterministic and invariant to
@@ -126,17 +126,17 @@ def test_philox_diag10_statistics_and_invariants(mode):
   assert 0.05 < acc < 0.6
 
   # determinism + sharding invariance on a short run with a trace
-  def run(n0, n1):
+  def run(n0, n1, spl=17):
     e = _engine(spec)
     e.init_chains(np.zeros((n1 - n0, 10)), chain_offset=n0)
     e.set_rng(mode, seed=99)
     e.alloc_trace(50, 1)
-    e.run(50, steps_per_launch=17)
+    e.run(50, steps_per_launch=spl)
     tr = e.trace()
     e.close()
     return tr
   full = run(0, 4096)
-  again = run(0, 4096)
+  again = run(0, 4096, spl=0)          # one launch == three launches
   lo, hi = run(0, 2048), run(2048, 4096)
   np.testing.assert_array_equal(full['v_x'], again['v_x'])
   np.testing.assert_array_equal(full['v_x'][:2048], lo['v_x'])
