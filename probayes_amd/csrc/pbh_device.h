@@ -36,7 +36,9 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
     const uint64_t p1 = (uint64_t)M1 * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    // three-input XORs as one v_bitop3_b32 each (truth table 0x96)
+    c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+              (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
     k0 += W0;
     k1 += W1;
   }

@@ -486,11 +486,23 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 // Lane-pair MH kernel for the sum-of-terms diagonal Gaussian with the
 // callable Gaussian delta (cfg2).  One chain per LANE PAIR (l, l + 32): lane
 // half h owns dims [h*H, h*H + H), H = D/2, so 65 536 chains fill 2 048
-// wavefronts = 2 per SIMD (the single-wave VALU issue limit halves throughput
-// at 1 wave/SIMD, MI355X_MICROARCH.md constants table).  The density keeps the
-// reference's left-to-right Python sum: half 0 sums its terms from 0 and hands
-// the partial to half 1 through v_permlane32_swap, half 1 finishes the sum,
-// scores, thresholds and hands the accept bit back.
+// wavefronts = 2 per SIMD (one wave alone issues at most one VALU per ~6
+// cycles, tools/ubench/isa_cost.hip; two interleaved waves reach the SIMD's
+// rate).  Half 1 holds the threshold and makes the chain's decision; the
+// accept bit returns to half 0 through a ballot (SALU mask ops, no VALU).
+//
+// Acceptance (all modes) is the reference's ratio form, sp_utils.py:40-64 +
+// pscales.py:56-65,219-236: s = min(1, exp_logp(lp') / max(tiny,
+// exp_logp(lp))), accept iff s >= t.  REPLAY evaluates it verbatim every
+// step.  The production modes evaluate the SAME decision through a filter:
+// e = 2^(fp32(log2e (lp' - lp))) on the hardware v_exp_f32 is within 2.7e-6
+// relative of s whenever |lp|, |lp'| <= 700 (no exp clamp or underflow in
+// the ratio form); t is known to 2^-24 from its leading word.  If t lies
+// outside [e (1 - 4e-6) - 2^-24, e (1 + 4e-6)] the decision is certain;
+// otherwise (about 1e-5 of chain-steps, and whenever the range test fails)
+// the lane evaluates the ratio form exactly with the libm-accurate exp and
+// an IEEE division, under a wave-uniform branch.  Decisions are therefore
+// those of the fp64 ratio form, at ~8 VALU instead of ~30.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t swap_u32(uint32_t v, bool hi) {
   const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
@@ -504,11 +516,57 @@ __device__ __forceinline__ double swap_f64(double v, bool hi) {
   return __builtin_bit_cast(double, lo | (up << 32));
 }
 
+// Ratio-form decision (sp_utils.py:40-64), evaluated exactly.
+__device__ __forceinline__ bool ratio_accept(double lpp, double lp, double t,
+                                            bool lin, double log_npi) {
+  const double eA = lin ? lpp : exp_logp(lpp, log_npi);
+  const double eB = lin ? lp : exp_logp(lp, log_npi);
+  double q = eA / np_max_tiny(eB);
+  q = q < 1. ? q : 1.;
+  return q >= t;
+}
+
+// Production draws of one half-step: H normals (fp32 Box-Muller pairs,
+// exact sign symmetry) and the two threshold words t0, t1
+// (t = u01(t0, t1), NumPy's 53-bit construction).  Philox blocks
+// j = q + 16 h per (step, chain); an odd pair count leaves the last block's
+// second half for the threshold, an even one takes block 0xFFFF.
+template <int H>
+__device__ __forceinline__ void pair_draw_philox(const KArgs &a, int h,
+                                                 int64_t g, int64_t chain,
+                                                 double (&r)[H], uint32_t &t0,
+                                                 uint32_t &t1) {
+  constexpr int P = (H + 1) / 2;
+#pragma unroll
+  for (int q = 0; q < (P + 1) / 2; ++q) {
+    const u32x4 w = philox4x32_10(ctr(q + 16 * h, g, chain), a.seed_lo, a.seed_hi);
+    double z1;
+    const double z0 = fast_normal_pair(w.x, w.z, z1);
+    if (4 * q < H) r[4 * q] = z0;
+    if (4 * q + 1 < H) r[4 * q + 1] = z1;
+    if (2 * q + 1 < P) {
+      double z3;
+      const double z2 = fast_normal_pair(w.y, w.w, z3);
+      if (4 * q + 2 < H) r[4 * q + 2] = z2;
+      if (4 * q + 3 < H) r[4 * q + 3] = z3;
+    } else {
+      t0 = w.y;
+      t1 = w.w;
+    }
+  }
+  if (P % 2 == 0) {
+    const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+    t0 = w.x;
+    t1 = w.y;
+  }
+}
+
 template <int D, int RNG>
 __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
   constexpr int H = D / 2;
   constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
+  constexpr bool REPLAY = RNG == PBH_RNG_REPLAY;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   const int lane = threadIdx.x & 63;
   const bool hi = lane >= 32;
@@ -518,6 +576,26 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   const bool active = c < a.n;
   const int64_t cc = active ? c : 0;
   const int k0 = h * H;   // first dim of this half
+  const uint64_t act_mask = __ballot(active);
+
+  // Per-lane model constants in VGPRs for the whole launch (the half's dims
+  // differ between lanes, so these are vector values, loaded once).
+  double psc[H], plc[H], ca[H], cb[H], cc2[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    psc[i] = a.pscl[k0 + i];
+    plc[i] = a.ploc[k0 + i];
+    if (FAST) {
+      // production density term u = x w - mu w, w = sqrt(0.5) / sigma
+      cb[i] = a.tw[k0 + i];
+      ca[i] = a.ta[k0 + i] * cb[i];
+      cc2[i] = 0.;
+    } else {
+      ca[i] = a.ta[k0 + i];   // norm_logpdf loc, scale, log(scale)
+      cb[i] = a.tb[k0 + i];
+      cc2[i] = a.tc[k0 + i];
+    }
+  }
 
   double x[H], ms[H], mq[H];
 #pragma unroll
@@ -527,8 +605,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     mq[i] = 0.;
   }
   double lp = a.lp[cc];
-  double eB = lin ? lp : (FAST ? exp_logp_fast(lp, a.log_npi)
-                              : exp_logp(lp, a.log_npi));
+  // REPLAY caches rescale(lp) (bit-identical to re-evaluating it)
+  double eB = REPLAY ? (lin ? lp : exp_logp(lp, a.log_npi)) : 0.;
   int64_t nacc = 0;
   const int64_t chain = a.off + cc;
   Xo xs{0u, 0u, 0u, 0u};
@@ -540,44 +618,17 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
 
-  // production draws of one step for this half: ceil(H/2) normal pairs, two
-  // pairs per Philox block; an odd pair count leaves the last block's second
-  // half for the 53-bit threshold (used by the upper half)
-  auto draw_fast = [&](int64_t gg, double (&rr)[H], double &tt) {
-    constexpr int P = (H + 1) / 2;
-#pragma unroll
-    for (int q = 0; q < (P + 1) / 2; ++q) {
-      const u32x4 w = philox4x32_10(ctr(q + 16 * h, gg, chain), a.seed_lo, a.seed_hi);
-      double z1;
-      const double z0 = fast_normal_pair(w.x, w.z, z1);
-      if (4 * q < H) rr[4 * q] = z0;
-      if (4 * q + 1 < H) rr[4 * q + 1] = z1;
-      if (2 * q + 1 < P) {
-        double z3;
-        const double z2 = fast_normal_pair(w.y, w.w, z3);
-        if (4 * q + 2 < H) rr[4 * q + 2] = z2;
-        if (4 * q + 3 < H) rr[4 * q + 3] = z3;
-      } else {
-        tt = u01(w.y, w.w);
-      }
-    }
-    if (P % 2 == 0) {
-      const u32x4 w = philox4x32_10(ctr(0xFFFFu, gg, chain), a.seed_lo, a.seed_hi);
-      tt = u01(w.x, w.y);
-    }
-  };
-  double rn[H], thrn = 0.;
-  if (RNG == PBH_RNG_PHILOX) draw_fast(a.g0, rn, thrn);
-
-  for (int s = 0; s < a.n_steps; ++s) {
+  // One chain-step.  (r, t0, t1) are this step's draws (production Philox:
+  // drawn one step ahead); (rn, n0, n1) receive the next step's.
+  auto step = [&](int s, double (&r)[H], uint32_t &t0, uint32_t &t1,
+                  double (&rn)[H], uint32_t &n0, uint32_t &n1) {
     const int64_t g = a.g0 + s;
-    double r[H];
     double thr = 0.;
-    if (RNG == PBH_RNG_REPLAY) {
+    if (REPLAY) {
       const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
 #pragma unroll
       for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
-      if (hi) thr = row[(int64_t)D * a.n];
+      thr = row[(int64_t)D * a.n];   // used by half 1
     } else if (RNG == PBH_RNG_XOSHIRO) {
       // this half's stream: two words per normal pair, then the threshold
       // (drawn by both halves so each stream advances the same per step)
@@ -589,17 +640,13 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
         r[2 * p] = fast_normal_pair(wu, wa, z1);
         if (2 * p + 1 < H) r[2 * p + 1] = z1;
       }
-      const uint32_t t0 = xo_next(xs);
-      thr = u01(t0, xo_next(xs));
-    } else if (FAST) {
-      // software-pipelined: this step's draws were generated last iteration
-      // (they do not depend on the chain state); issue the next step's
-      // Philox blocks now so they overlap this step's fp64 chain.
-#pragma unroll
-      for (int i = 0; i < H; ++i) r[i] = rn[i];
-      thr = thrn;
-      draw_fast(g + 1, rn, thrn);
-    } else {
+      t0 = xo_next(xs);
+      t1 = xo_next(xs);
+    } else if (RNG == PBH_RNG_PHILOX) {
+      // software-pipelined: issue the next step's Philox blocks now so they
+      // overlap this step's fp64 chain (the draws never depend on state)
+      pair_draw_philox<H>(a, h, g + 1, chain, rn, n0, n1);
+    } else {   // PHILOX_F64: fp64 Box-Muller
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
         double z0, z1;
@@ -607,80 +654,108 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
         r[2 * p] = z0;
         if (2 * p + 1 < H) r[2 * p + 1] = z1;
       }
-      if (hi) {
-        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
-        thr = u01(w.x, w.y);
-      }
+      const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+      t0 = w.x;
+      t1 = w.y;
     }
     // proposal of this half's dims (scipy rvs: z * scale + loc)
     double xp[H];
 #pragma unroll
     for (int i = 0; i < H; ++i)
-      xp[i] = x[i] + (r[i] * cld(a.pscl, k0 + i) + cld(a.ploc, k0 + i));
+      xp[i] = FAST ? x[i] + __builtin_fma(r[i], psc[i], plc[i])
+                   : x[i] + (r[i] * psc[i] + plc[i]);
     // density: Python sum from 0, dims in order, split across the pair
     double lpp;
     if (FAST) {
-      // production path: each half sums -(w (x - mu))^2 over its dims; the
-      // order of the fp64 sum is free here (no reference stream to match)
-      double part = 0.0;
+      // production: -sum (x w - mu w)^2 - ksum; order of the sum is free
+      double p0 = 0., p1 = 0.;
 #pragma unroll
       for (int i = 0; i < H; ++i) {
-        const double u = (xp[i] - cld(a.ta, k0 + i)) * cld(a.tw, k0 + i);
-        part = __builtin_fma(-u, u, part);
+        const double u = __builtin_fma(xp[i], cb[i], -ca[i]);
+        if (i & 1) p1 = __builtin_fma(u, u, p1);
+        else p0 = __builtin_fma(u, u, p0);
       }
-      lpp = (part + swap_f64(part, hi)) - a.ksum;
+      const double part = p0 + p1;
+      lpp = -((part + swap_f64(part, hi)) + a.ksum);
     } else {
+      double tm[H];
 #pragma unroll
       for (int i = 0; i < H; ++i)
-        r[i] = norm_logpdf(xp[i], cld(a.ta, k0 + i), cld(a.tb, k0 + i),
-                           cld(a.tc, k0 + i), a.norm_logC);  // terms
+        tm[i] = norm_logpdf(xp[i], ca[i], cb[i], cc2[i], a.norm_logC);
       double s0 = 0.0;
 #pragma unroll
-      for (int i = 0; i < H; ++i) s0 = s0 + (hi ? 0.0 : r[i]);
-      const double from_lo = swap_f64(s0, hi);   // half 1 gets half 0's sum
-      lpp = from_lo;
+      for (int i = 0; i < H; ++i) s0 = s0 + (hi ? 0.0 : tm[i]);
+      lpp = swap_f64(s0, hi);   // half 1 gets half 0's sum
 #pragma unroll
-      for (int i = 0; i < H; ++i) lpp = lpp + r[i];
+      for (int i = 0; i < H; ++i) lpp = lpp + tm[i];
     }
     // half 1 holds the full density and the threshold: its decision is the
     // chain's (computed branch-free in both halves; half 0's is discarded)
-    const double eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
-                                        : exp_logp(lpp, a.log_npi));
-    double q = eA / np_max_tiny(eB);
-    q = q < 1. ? q : 1.;
     const bool first = !a.has_pred && s == 0;   // s = None on step 1
-    const uint32_t acc_bit = (first || q >= thr) ? 1u : 0u;
-    const uint32_t acc_lo = swap_u32(acc_bit, hi);   // half 0 receives it
-    const bool acc = (hi ? acc_bit : acc_lo) != 0;
+    bool acc;
+    double eA = 0.;
+    if (REPLAY) {
+      eA = lin ? lpp : exp_logp(lpp, a.log_npi);
+      double q = eA / np_max_tiny(eB);
+      q = q < 1. ? q : 1.;
+      acc = first || q >= thr;
+    } else {
+      const float e = __builtin_amdgcn_exp2f(
+          (float)((lpp - lp) * 1.4426950408889634));
+      const float tlo = (float)(t0 >> 8) * 5.9604644775390625e-08f;   // 2^-24
+      const float thi = tlo + 5.9604644775390625e-08f;
+      const bool inr = !lin && __builtin_fabs(lpp) <= 700. &&
+                       __builtin_fabs(lp) <= 700.;
+      const bool af = thi <= e * 0.999996f;
+      const bool rf = tlo > e * 1.000004f;
+      acc = first || (inr && af);
+      const bool need = hi && !first && !(inr && (af || rf));
+      if (__ballot(need)) {   // wave-uniform, rare
+        if (need) acc = ratio_accept(lpp, lp, u01(t0, t1), lin, a.log_npi);
+      }
+    }
+    // half 1's decision is the chain's: lanes l and l + 32 both take bit
+    // l + 32 of the ballot (SGPR mask ops; inverse_ballot feeds v_cndmask)
+    const uint64_t mhi = __ballot(hi && acc) & 0xFFFFFFFF00000000ull;
+    const bool accl = __builtin_amdgcn_inverse_ballot_w64(mhi | (mhi >> 32));
 #pragma unroll
-    for (int i = 0; i < H; ++i) x[i] = acc ? xp[i] : x[i];
-    lp = (acc && hi) ? lpp : lp;
-    eB = (acc && hi) ? eA : eB;
-    nacc += acc ? 1 : 0;
+    for (int i = 0; i < H; ++i) x[i] = accl ? xp[i] : x[i];
+    if (REPLAY) eB = accl ? eA : eB;
+    lp = accl ? lpp : lp;
+    nacc += accl ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < H; ++i) {
       ms[i] += x[i];
-      mq[i] += x[i] * x[i];
+      mq[i] = __builtin_fma(x[i], x[i], mq[i]);
     }
     const bool rec_now = ph == 0;
     const int64_t rec = ri;
     ph = (ph + 1 == a.thin) ? 0 : ph + 1;   // next step's phase
     ri += (ph == 0) ? 1 : 0;
-    if (rec_now) {
-      if (rec >= 0 && rec < a.rec_cap) {
-        if (active) {
+    if (rec_now && rec >= 0 && rec < a.rec_cap) {
+      double *row = a.tx + rec * D * a.n;
+      if (active) {
 #pragma unroll
-          for (int i = 0; i < H; ++i) a.tx[(rec * D + k0 + i) * a.n + c] = x[i];
-          if (hi) a.tlp[rec * a.n + c] = lp;
-        }
-        // 32 chains per wave: the upper half's ballot bits are the mask word
-        const uint64_t mask = __ballot(active && acc && hi) >> 32;
-        if (lane == 32 && (c >> 5) < 2 * a.W)
-          reinterpret_cast<uint32_t *>(a.tacc)[rec * 2 * a.W + (c >> 5)] =
-              (uint32_t)mask;
+        for (int i = 0; i < H; ++i) row[(k0 + i) * a.n + c] = x[i];
+        if (hi) a.tlp[rec * a.n + c] = lp;
       }
+      // 32 chains per wave: the upper half's ballot bits are the mask word
+      if (lane == 32 && (c >> 5) < 2 * a.W)
+        reinterpret_cast<uint32_t *>(a.tacc)[rec * 2 * a.W + (c >> 5)] =
+            (uint32_t)((mhi & act_mask) >> 32);
     }
+  };
+
+  double rA[H], rB[H];
+  uint32_t tA0 = 0, tA1 = 0, tB0 = 0, tB1 = 0;
+  if (RNG == PBH_RNG_PHILOX) pair_draw_philox<H>(a, h, a.g0, chain, rA, tA0, tA1);
+  int s = 0;
+  for (; s + 1 < a.n_steps; s += 2) {   // ping-pong the pipelined draws
+    step(s, rA, tA0, tA1, rB, tB0, tB1);
+    step(s + 1, rB, tB0, tB1, rA, tA0, tA1);
   }
+  if (s < a.n_steps) step(s, rA, tA0, tA1, rB, tB0, tB1);
+
   if (active) {
 #pragma unroll
     for (int i = 0; i < H; ++i) {

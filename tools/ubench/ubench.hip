@@ -61,6 +61,55 @@ __global__ void k_expcheck(double *out, const double *x, int n) {
   if (i < n) { out[2 * i] = exp(x[i]); out[2 * i + 1] = fast_exp(x[i]); }
 }
 
+__global__ void k_mullo(uint32_t *out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x, c = a ^ 7, d = b + 3;
+  for (int i = 0; i < R; ++i) {
+    a = a * 0xD2511F53u + s; b = b * 0xCD9E8D57u + s; c = c * 0xD2511F53u + s; d = d * 0xCD9E8D57u + s;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a ^ b ^ c ^ d;
+}
+__global__ void k_mulhi(uint32_t *out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x, c = a ^ 7, d = b + 3;
+  for (int i = 0; i < R; ++i) {
+    a = __umulhi(a, 0xD2511F53u) ^ s; b = __umulhi(b, 0xCD9E8D57u) ^ s; c = __umulhi(c, 0xD2511F53u) ^ s; d = __umulhi(d, 0xCD9E8D57u) ^ s;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a ^ b ^ c ^ d;
+}
+__global__ void k_xor3(uint32_t *out, uint32_t s) {
+  uint32_t a = threadIdx.x + s, b = blockIdx.x, c = a ^ 7, d = b + 3;
+  for (int i = 0; i < R; ++i) {
+    a = a ^ b ^ s; b = b ^ c ^ s; c = c ^ d ^ s; d = d ^ a ^ s;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a ^ b ^ c ^ d;
+}
+__global__ void k_add64(double *out, double s) {
+  double a = threadIdx.x * s, b = blockIdx.x * s, c = a + 1, d = b + 1;
+  for (int i = 0; i < R; ++i) { a = a + s; b = b + s; c = c + s; d = d + s; }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a + b + c + d;
+}
+__global__ void k_trans32(float *out, float s) {
+  float a = threadIdx.x * s, b = blockIdx.x * s, c = a + 1, d = b + 1;
+  for (int i = 0; i < R; ++i) {
+    a = __builtin_amdgcn_logf(a); b = __builtin_amdgcn_logf(b); c = __builtin_amdgcn_logf(c); d = __builtin_amdgcn_logf(d);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a + b + c + d;
+}
+__global__ void k_cvt(double *out, double s) {
+  float a = threadIdx.x * (float)s, b = blockIdx.x, c = a + 1, d = b + 1;
+  double acc = 0;
+  for (int i = 0; i < R; ++i) {
+    double x = (double)a, y = (double)b, z = (double)c, w = (double)d;
+    a = (float)x + 1.f; b = (float)y + 1.f; c = (float)z + 1.f; d = (float)w + 1.f;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a + b + c + d;
+}
+__global__ void k_xoshiro(uint32_t *out, uint32_t s) {
+  Xo x{threadIdx.x + s, blockIdx.x | 1u, s, 7u};
+  uint32_t acc = 0;
+  for (int i = 0; i < R / 4; ++i) acc ^= xo_next(x);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 template <class K, class T>
 float timeit(K k, T *buf, T s, int blocks) {
   hipEvent_t e0, e1;
@@ -88,6 +137,14 @@ int main() {
   rep("xor+add", timeit(k_xor, u, 3u, blocks), 4 * 2, R);
   rep("fma_f64", timeit(k_fma64, d, 0.999, blocks), 4, R);
   rep("fma_f32", timeit(k_fma32, f, 0.999f, blocks), 4, R);
+  rep("mul_lo", timeit(k_mullo, u, 3u, blocks), 4 * 2, R);
+  rep("mul_hi+x", timeit(k_mulhi, u, 3u, blocks), 4 * 2, R);
+  rep("xor3", timeit(k_xor3, u, 3u, blocks), 4, R);
+  rep("add_f64", timeit(k_add64, d, 0.999, blocks), 4, R);
+  rep("log_f32", timeit(k_trans32, f, 0.999f, blocks), 4, R);
+  rep("cvt64+32+a", timeit(k_cvt, d, 0.999, blocks), 4 * 3, R);
+  float xm = timeit(k_xoshiro, u, 3u, blocks);
+  printf("xoshiro   %8.3f ms  %.1f ns per word per wave-slot\n", xm, xm * 1e6 / (waves * R / 4) * simds);
   float pm = timeit(k_philox, u, 3u, blocks);
   printf("philox    %8.3f ms  %.1f ns per call per wave-slot\n", pm, pm * 1e6 / (waves * R / 16) * simds);
   float em = timeit(k_exp64, d, 0.5, blocks);
