@@ -194,6 +194,15 @@ int pbh_rccl_allgather_moments(pbh_engine *eng, double *out);
 int pbh_rccl_allreduce_max(pbh_engine *eng, double *value);
 int pbh_rccl_destroy(pbh_engine *eng);
 
+/* ---- diagnostics -------------------------------------------------------- */
+/* Evaluates the production-mode acceptance filter and the exact ratio form
+ * (sp_utils.py:40-64) on device for n triples (lp, lp', t = u01(t0, t1)).
+ * out[i]: bit 0 = exact decision s >= t, bit 1 = the filter decided without
+ * the exact fallback, bit 2 = the filter's decision.                        */
+int pbh_check_accept(int device, int64_t n, const double *lp,
+                     const double *lpp, const uint32_t *t0, const uint32_t *t1,
+                     int32_t lin, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,7 @@ RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2, 'xoshiro': 3}
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 
@@ -95,6 +96,8 @@ SIGNATURES = {
     'pbh_rccl_allgather_moments': (ctypes.c_int, [ctypes.c_void_p, _dp]),
     'pbh_rccl_allreduce_max': (ctypes.c_int, [ctypes.c_void_p, _dp]),
     'pbh_rccl_destroy': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_check_accept': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _dp, _dp,
+                                        _u32p, _u32p, ctypes.c_int32, _u8p]),
 }
 
 

@@ -337,4 +337,41 @@ __device__ __forceinline__ double np_max_tiny(double b) {
   return (b != b) ? b : (b >= kNearlyPosZero ? b : kNearlyPosZero);
 }
 
+// ---------------------------------------------------------------------------
+// MH acceptance (sp_utils.py:40-64, pscales.py:56-65,219-236): the
+// reference's ratio form s = min(1, exp_logp(lp') / max(tiny, exp_logp(lp))),
+// accept iff s >= t.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool ratio_accept(double lpp, double lp, double t,
+                                            bool lin, double log_npi) {
+  const double eA = lin ? lpp : exp_logp(lpp, log_npi);
+  const double eB = lin ? lp : exp_logp(lp, log_npi);
+  double q = eA / np_max_tiny(eB);
+  q = q < 1. ? q : 1.;
+  return q >= t;
+}
+
+// The same decision through a cheap filter (production RNG modes).  With
+// t = u01(t0, t1), t lies in [tlo, tlo + 2^-24), tlo = (t0 >> 8) 2^-24.
+// e = 2^(fp32(log2e (lp' - lp))) on v_exp_f32 is within 2.7e-6 relative of
+// s whenever |lp|, |lp'| <= 700 (then no exp clamp, overflow or underflow
+// occurs in the ratio form): fp32 rounding of the argument (|y| <= 60 where
+// it matters) costs 4.2e-8 |y|, v_exp_f32 1 ulp.  So t < e (1 - 4e-6)
+// proves accept and t > e (1 + 4e-6) proves reject; otherwise `need` is set
+// and the caller must evaluate ratio_accept (about 1e-5 of chain-steps).
+struct Decision { bool acc, need; };
+
+__device__ __forceinline__ Decision accept_filter(double lpp, double lp,
+                                                  uint32_t t0, bool lin) {
+  const float e = __builtin_amdgcn_exp2f(
+      (float)((lpp - lp) * 1.4426950408889634));
+  const float tlo = (float)(t0 >> 8) * 5.9604644775390625e-08f;   // 2^-24
+  const float thi = tlo + 5.9604644775390625e-08f;
+  const bool inr = !lin && __builtin_fabs(lpp) <= 700. &&
+                   __builtin_fabs(lp) <= 700.;
+  const bool af = thi <= e * 0.999996f;
+  const bool rf = tlo > e * 1.000004f;
+  return Decision{inr && af, !(inr && (af || rf))};
+}
+
 }  // namespace pbh

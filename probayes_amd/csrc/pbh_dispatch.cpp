@@ -75,4 +75,27 @@ hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
   return hipGetLastError();
 }
 
+// Diagnostic: the production acceptance filter against the exact ratio form
+// on caller-supplied (lp, lp', t) triples.  out[i] bit 0 = exact decision,
+// bit 1 = the filter decided (no fallback needed), bit 2 = filter decision.
+__global__ void check_accept_kernel(int64_t n, const double *lp,
+                                    const double *lpp, const uint32_t *t0,
+                                    const uint32_t *t1, int32_t lin,
+                                    double log_npi, uint8_t *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double t = u01(t0[i], t1[i]);
+  const bool ex = ratio_accept(lpp[i], lp[i], t, lin != 0, log_npi);
+  const Decision d = accept_filter(lpp[i], lp[i], t0[i], lin != 0);
+  out[i] = (uint8_t)((ex ? 1 : 0) | (d.need ? 0 : 2) | (d.acc ? 4 : 0));
+}
+
+hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
+                               const uint32_t *t0, const uint32_t *t1,
+                               int32_t lin, double log_npi, uint8_t *out) {
+  hipLaunchKernelGGL(check_accept_kernel, dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, 0, n, lp, lpp, t0, t1, lin, log_npi, out);
+  return hipGetLastError();
+}
+
 }  // namespace pbh

@@ -790,4 +790,38 @@ int pbh_rccl_destroy(pbh_engine *e) {
   return PBH_OK;
 }
 
+int pbh_check_accept(int device, int64_t n, const double *lp,
+                     const double *lpp, const uint32_t *t0, const uint32_t *t1,
+                     int32_t lin, uint8_t *out) {
+  if (check_ptr(lp, "lp") || check_ptr(lpp, "lpp") || check_ptr(t0, "t0") ||
+      check_ptr(t1, "t1") || check_ptr(out, "out"))
+    return PBH_ERR_ARG;
+  if (n <= 0) return fail(PBH_ERR_ARG, "n must be positive");
+  HIP_TRY(hipSetDevice(device));
+  double *dlp = nullptr, *dlpp = nullptr;
+  uint32_t *d0 = nullptr, *d1 = nullptr;
+  uint8_t *dout = nullptr;
+  int rc = dalloc(dlp, n);
+  if (!rc) rc = dalloc(dlpp, n);
+  if (!rc) rc = dalloc(d0, n);
+  if (!rc) rc = dalloc(d1, n);
+  if (!rc) rc = dalloc(dout, n);
+  hipError_t err = hipSuccess;
+  if (!rc) {
+    err = hipMemcpy(dlp, lp, n * sizeof(double), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(dlpp, lpp, n * sizeof(double), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(d0, t0, n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(d1, t1, n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess)
+      err = pbh::launch_check_accept(n, dlp, dlpp, d0, d1, lin,
+                                     std::log(1.7976931348623158e+308), dout);
+    if (err == hipSuccess) err = hipMemcpy(out, dout, n, hipMemcpyDeviceToHost);
+  }
+  dfree(dlp); dfree(dlpp); dfree(d0); dfree(d1); dfree(dout);
+  if (rc) return rc;
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_check_accept: %s", hipGetErrorString(err));
+  return PBH_OK;
+}
+
 }  // extern "C"

@@ -516,16 +516,6 @@ __device__ __forceinline__ double swap_f64(double v, bool hi) {
   return __builtin_bit_cast(double, lo | (up << 32));
 }
 
-// Ratio-form decision (sp_utils.py:40-64), evaluated exactly.
-__device__ __forceinline__ bool ratio_accept(double lpp, double lp, double t,
-                                            bool lin, double log_npi) {
-  const double eA = lin ? lpp : exp_logp(lpp, log_npi);
-  const double eB = lin ? lp : exp_logp(lp, log_npi);
-  double q = eA / np_max_tiny(eB);
-  q = q < 1. ? q : 1.;
-  return q >= t;
-}
-
 // Production draws of one half-step: H normals (fp32 Box-Muller pairs,
 // exact sign symmetry) and the two threshold words t0, t1
 // (t = u01(t0, t1), NumPy's 53-bit construction).  Philox blocks
@@ -700,16 +690,9 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       q = q < 1. ? q : 1.;
       acc = first || q >= thr;
     } else {
-      const float e = __builtin_amdgcn_exp2f(
-          (float)((lpp - lp) * 1.4426950408889634));
-      const float tlo = (float)(t0 >> 8) * 5.9604644775390625e-08f;   // 2^-24
-      const float thi = tlo + 5.9604644775390625e-08f;
-      const bool inr = !lin && __builtin_fabs(lpp) <= 700. &&
-                       __builtin_fabs(lp) <= 700.;
-      const bool af = thi <= e * 0.999996f;
-      const bool rf = tlo > e * 1.000004f;
-      acc = first || (inr && af);
-      const bool need = hi && !first && !(inr && (af || rf));
+      const Decision dc = accept_filter(lpp, lp, t0, lin);
+      acc = first || dc.acc;
+      const bool need = hi && !first && dc.need;
       if (__ballot(need)) {   // wave-uniform, rare
         if (need) acc = ratio_accept(lpp, lp, u01(t0, t1), lin, a.log_npi);
       }
