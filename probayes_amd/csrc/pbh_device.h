@@ -113,6 +113,21 @@ __device__ __forceinline__ double fast_normal_pair(uint32_t wu, uint32_t wa,
   return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, (double)c) ^ s0);
 }
 
+// One production normal from two words (the cosine half of fast_normal_pair),
+// for odd per-lane draw counts.  Bits used: wu[31:8], wa[31:8], wa[0]; the
+// 14 bits wu[7:0], wa[6:1] are returned in spare (independent of the normal).
+__device__ __forceinline__ double fast_normal_single(uint32_t wu, uint32_t wa,
+                                                     uint32_t &spare) {
+  const float u1 = (float)((wu >> 8) + 1u) * 5.9604644775390625e-08f;  // 2^-24
+  const float rev = (float)(wa >> 8) * 1.4901161193847656e-08f;      // [0, 1/4)
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f *
+                                         __builtin_amdgcn_logf(u1));
+  const float c = r * __builtin_amdgcn_cosf(rev);
+  spare = ((wu & 0xFFu) << 6) | ((wa >> 1) & 0x3Fu);
+  const uint64_t s0 = (uint64_t)(wa & 1u) << 63;
+  return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, (double)c) ^ s0);
+}
+
 // a / b for a loop-invariant b with its reciprocal rb = 1/b: one FMA
 // correction of a*rb (Markstein) -- the correctly rounded quotient in all but
 // rare ties; used only on the production path (parity paths divide).
@@ -224,7 +239,7 @@ __device__ double np_pairwise(F f, int64_t n) {
 // 1.15 ships; the coefficients below reproduce scipy's ndtri bit-for-bit on
 // the host (tests/test_device_math.py) -- on the device up to log/sqrt ulps.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double ndtri(double y0) {
+__host__ __device__ inline double ndtri(double y0) {
   constexpr double s2pi = 2.50662827463100050242E0;
   constexpr double P0[5] = {-5.99633501014107895267E1, 9.80010754185999661536E1,
                             -5.66762857469070293439E1, 1.39312609387279679503E1,
@@ -361,17 +376,28 @@ __device__ __forceinline__ bool ratio_accept(double lpp, double lp, double t,
 // and the caller must evaluate ratio_accept (about 1e-5 of chain-steps).
 struct Decision { bool acc, need; };
 
-__device__ __forceinline__ Decision accept_filter(double lpp, double lp,
-                                                  uint32_t t0, bool lin) {
+// LB = number of leading bits of t known to the filter: t lies in
+// [lead 2^-LB, (lead + 1) 2^-LB).  The lane-pair kernel's Philox path packs a
+// 14-bit lead beside its normals (its fallback draws the remaining bits).
+template <int LB>
+__device__ __forceinline__ Decision accept_filter_lead(double lpp, double lp,
+                                                       uint32_t lead, bool lin) {
+  constexpr float w = 1.0f / (float)(1u << LB);
   const float e = __builtin_amdgcn_exp2f(
       (float)((lpp - lp) * 1.4426950408889634));
-  const float tlo = (float)(t0 >> 8) * 5.9604644775390625e-08f;   // 2^-24
-  const float thi = tlo + 5.9604644775390625e-08f;
+  const float tlo = (float)lead * w;
+  const float thi = tlo + w;
   const bool inr = !lin && __builtin_fabs(lpp) <= 700. &&
                    __builtin_fabs(lp) <= 700.;
   const bool af = thi <= e * 0.999996f;
   const bool rf = tlo > e * 1.000004f;
   return Decision{inr && af, !(inr && (af || rf))};
+}
+
+// t = u01(t0, t1): the lead is t0's top 24 bits.
+__device__ __forceinline__ Decision accept_filter(double lpp, double lp,
+                                                  uint32_t t0, bool lin) {
+  return accept_filter_lead<24>(lpp, lp, t0 >> 8, lin);
 }
 
 }  // namespace pbh

@@ -17,6 +17,7 @@
 
 #include "../../include/pbhip.h"
 #include "pbh_kernels.h"
+#include "pbh_device.h"
 
 using pbh::KArgs;
 
@@ -55,6 +56,14 @@ struct pbh_engine {
   int64_t mom_steps = 0;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
+  bool gibbs_fast = true;    // PBH_GIBBS_FAST=0 keeps the ndtri kernel for Philox
+  int gibbs_lanes = 0;       // PBH_GIBBS_LANES: lanes per chain of that kernel
+  // MVN target on the host (for the production Gibbs tables)
+  std::vector<double> mvn_mean, mvn_U;
+  double mvn_const = 0.;
+  // production Gibbs: persisted g = P'(x - mu'), Q per chain
+  double *gq = nullptr;
+  bool gq_valid = false;
   // timing of the last pbh_run
   bool timed = false;
   int64_t last_launches = 0;
@@ -170,6 +179,8 @@ int pbh_create(int device, pbh_engine **out) {
   e->device = device;
   if (const char *np = std::getenv("PBH_NO_PAIR")) e->pair_enabled = np[0] != '1';
   if (const char *gm = std::getenv("PBH_GIBBS_MFMA")) e->gibbs_mfma = gm[0] != '0';
+  if (const char *gf = std::getenv("PBH_GIBBS_FAST")) e->gibbs_fast = gf[0] != '0';
+  if (const char *gl = std::getenv("PBH_GIBBS_LANES")) e->gibbs_lanes = std::atoi(gl);
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -188,7 +199,7 @@ int pbh_destroy(pbh_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
-  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo);
+  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq);
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
@@ -324,6 +335,14 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
   k.log_npi = std::log(1.7976931348623158e+308);
   k.norm_C = std::sqrt(2 * M_PI);
   k.norm_logC = std::log(k.norm_C);
+  if (m->target_kind == PBH_TARGET_MVN) {
+    e->mvn_mean.assign(A, A + d);
+    e->mvn_U.assign(B, B + (size_t)d * d);
+    e->mvn_const = C[0];
+  } else {
+    e->mvn_mean.clear();
+    e->mvn_U.clear();
+  }
   e->d = d;
   e->has_model = true;
   return PBH_OK;
@@ -393,13 +412,55 @@ int pbh_set_gibbs(pbh_engine *e, const pbh_gibbs *gb) {
   const size_t oc = pack(blk, gb->coef ? gb->coef : gb->mean, d > 1 ? (int64_t)d * (d - 1) : 0);
   const size_t os = pack(blk, gb->stdv, d);
   const size_t ocdf = pack(blk, gb->cdf, 2 * d);
+  // Production-kernel tables (gibbs_fast_kernel).  The density is taken at
+  // y = x[perm] (prob.py:354-357): P = U U^T in y order; re-indexed to x
+  // order P'[j][j'] = P[inv(j)][inv(j')], mu'[j] = mean[inv(j)].  z limits
+  // are ndtri of the cdf limits (the truncation cond_cov.py:57-62 applies).
+  std::vector<int> inv(d);
+  for (int i = 0; i < d; ++i) {
+    const int pi = d <= 1 ? 0 : (d == 2 ? 1 - i : (i < d - 1 ? d - 2 - i : d - 1));
+    inv[pi] = i;
+  }
+  std::vector<double> pp((size_t)d * d), mup(d), zlo(d), zhi(d);
+  for (int j = 0; j < d; ++j) {
+    mup[j] = e->mvn_mean[inv[j]];
+    for (int jj = 0; jj < d; ++jj) {
+      double acc = 0.;
+      for (int o = 0; o < d; ++o)
+        acc += e->mvn_U[(size_t)inv[j] * d + o] * e->mvn_U[(size_t)inv[jj] * d + o];
+      pp[(size_t)j * d + jj] = acc;
+    }
+  }
+  for (int j = 0; j < d; ++j) {
+    zlo[j] = pbh::ndtri(gb->cdf[2 * j]);
+    zhi[j] = pbh::ndtri(gb->cdf[2 * j + 1]);
+  }
+  std::vector<double> ak(d);
+  for (int k = 0; k < d; ++k) {
+    double acc = 0.;
+    for (int i = 0, jj = 0; i < d; ++i) {
+      if (i == k) continue;
+      acc += gb->coef[(size_t)k * (d - 1) + jj++] * gb->mean[i];
+    }
+    ak[k] = gb->mean[k] - acc;
+  }
+  const size_t oak = pack(blk, ak.data(), d);
+  const size_t opp = pack(blk, pp.data(), (int64_t)d * d);
+  const size_t omup = pack(blk, mup.data(), d);
+  const size_t ozlo = pack(blk, zlo.data(), d);
+  const size_t ozhi = pack(blk, zhi.data(), d);
   HIP_TRY(hipSetDevice(e->device));
   int rc = upload(e->dgibbs, blk, e->stream);
   if (rc) return rc;
   KArgs &k = e->k;
   k.gmean = e->dgibbs + om; k.gcoef = e->dgibbs + oc;
   k.gstdv = e->dgibbs + os; k.gcdf = e->dgibbs + ocdf;
+  k.gpp = e->dgibbs + opp; k.gmup = e->dgibbs + omup;
+  k.gzlo = e->dgibbs + ozlo; k.gzhi = e->dgibbs + ozhi;
+  k.gak = e->dgibbs + oak;
+  k.gconst = e->mvn_const;
   k.tsteps = gb->tsteps;
+  e->gq_valid = false;
   k.prop = PBH_PROP_GIBBS;
   e->draw_order.assign(gb->tsteps, 0);
   for (int i = 0; i < gb->tsteps; ++i) e->draw_order[i] = i;
@@ -426,8 +487,10 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
     if (!rc) rc = dalloc(e->msq, (size_t)n * d);
     if (!rc) rc = dalloc(e->nacc, n);
     if (!rc) rc = dalloc(e->xo, (size_t)8 * n);
+    if (!rc) rc = dalloc(e->gq, (size_t)(d + 1) * n);
     if (rc) return rc;
   }
+  e->gq_valid = false;
   std::vector<double> xt((size_t)n * d);
   for (int64_t c = 0; c < n; ++c)
     for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = init[(size_t)c * d + k];
@@ -589,6 +652,10 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     k.pair_ok = (e->pair_enabled && (k.scores == PBH_SCORES_METROPOLIS || qt > 0.0)) ? 1 : 0;
   }
   k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
+  k.gibbs_fast = e->gibbs_fast ? 1 : 0;
+  k.gibbs_lanes = e->gibbs_lanes;
+  k.gq = e->gq;
+  const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
                       k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
@@ -601,12 +668,14 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     k.g0 = e->g;
     k.has_pred = e->has_pred ? 1 : 0;
     k.rep_row0 = e->g - e->rep_g0;
+    k.gq_init = e->gq_valid ? 0 : 1;
     hipError_t err = e->has_gibbs ? pbh::launch_gibbs(k, e->stream)
                                   : pbh::launch_mh(k, e->stream, lds);
     if (err != hipSuccess)
       return fail(PBH_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(err));
     e->g += m;
     e->has_pred = true;
+    e->gq_valid = gfast;   // only the production Gibbs kernel maintains g, Q
     done += m;
     ++launches;
   }

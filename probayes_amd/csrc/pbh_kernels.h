@@ -59,10 +59,26 @@ struct KArgs {
   int64_t W;         // accept-mask words per recorded step = ceil(n / 64)
   int32_t pair_ok;   // engine allows the lane-pair kernel (see launch_mh_d)
   int32_t gibbs_mfma;  // Gibbs density quadratic form on MFMA (d <= 16)
+  // ---- production CondCov Gibbs (gibbs_fast_kernel) ----
+  int32_t gibbs_fast;  // engine allows the production Gibbs kernel
+  const double *gpp;   // precision of the permuted density in x order [d][d]
+  const double *gmup;  // mean of the permuted density in x order [d]
+  const double *gzlo, *gzhi;  // ndtri(cdf limits): truncation of z per dim
+  const double *gak;   // a_k = mean_k - coef_k . mean_-k
+  double gconst;       // rank * log(2 pi) + log_pdet
+  double *gq;          // persisted g = P'(x - mu') [d][n] and Q [n]
+  int32_t gq_init;     // 1: recompute g, Q from x at entry
+  int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
   // ---- moments ----
   double *msum, *msq;
   int64_t *nacc;
 };
+
+// The production Gibbs kernel runs for the Philox RNG without debug records,
+// d <= 16 (its per-lane constant block grows as d^2).
+inline bool gibbs_fast_form(const KArgs &a) {
+  return a.gibbs_fast && a.rng == 1 /* PBH_RNG_PHILOX */ && !a.debug && a.d <= 16;
+}
 
 // Host launchers (pbh_kernels.hip).
 hipError_t launch_mh(const KArgs &a, hipStream_t s, size_t lds_bytes);

@@ -14,6 +14,8 @@
 //   -> score (sp_utils.py:19-64) -> s >= t (sp_utils.py:34-37)
 //   -> keep (x', p') on accept else (x, p)  (sp.py:253-256)
 #pragma once
+#include <utility>
+
 #include "pbh_kernels.h"
 #include "pbh_device.h"
 #include "../../include/pbhip.h"
@@ -516,38 +518,40 @@ __device__ __forceinline__ double swap_f64(double v, bool hi) {
   return __builtin_bit_cast(double, lo | (up << 32));
 }
 
-// Production draws of one half-step: H normals (fp32 Box-Muller pairs,
-// exact sign symmetry) and the two threshold words t0, t1
-// (t = u01(t0, t1), NumPy's 53-bit construction).  Philox blocks
-// j = q + 16 h per (step, chain); an odd pair count leaves the last block's
-// second half for the threshold, an even one takes block 0xFFFF.
+// Production draws of a PAIR of half-steps (steps 2P, 2P + 1) of one lane:
+// NP = H / 2 Box-Muller pairs per step from NP Philox blocks (q < NP), and
+// one more block q = NP holding the odd normal of each step (H odd; its
+// spare bits carry the step's 14-bit threshold lead) or the two threshold
+// leads (H even, 24 bits).  3 blocks per 2 steps at H = 5 instead of 4, and
+// 2.5 Box-Muller evaluations per step instead of 3.
 template <int H>
-__device__ __forceinline__ void pair_draw_philox(const KArgs &a, int h,
-                                                 int64_t g, int64_t chain,
-                                                 double (&r)[H], uint32_t &t0,
-                                                 uint32_t &t1) {
-  constexpr int P = (H + 1) / 2;
+__device__ __forceinline__ void pair2_draw_philox(const KArgs &a, int h,
+                                                  int64_t P, int64_t chain,
+                                                  double (&ra)[H], double (&rb)[H],
+                                                  uint32_t &ta, uint32_t &tb) {
+  constexpr int NP = H / 2;
 #pragma unroll
-  for (int q = 0; q < (P + 1) / 2; ++q) {
-    const u32x4 w = philox4x32_10(ctr(q + 16 * h, g, chain), a.seed_lo, a.seed_hi);
-    double z1;
-    const double z0 = fast_normal_pair(w.x, w.z, z1);
-    if (4 * q < H) r[4 * q] = z0;
-    if (4 * q + 1 < H) r[4 * q + 1] = z1;
-    if (2 * q + 1 < P) {
-      double z3;
-      const double z2 = fast_normal_pair(w.y, w.w, z3);
-      if (4 * q + 2 < H) r[4 * q + 2] = z2;
-      if (4 * q + 3 < H) r[4 * q + 3] = z3;
-    } else {
-      t0 = w.y;
-      t1 = w.w;
+  for (int q = 0; q < NP; ++q) {
+    const u32x4 w = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+    double z0, z1, z2, z3;
+    z0 = fast_normal_pair(w.x, w.z, z1);
+    z2 = fast_normal_pair(w.y, w.w, z3);
+    // global pairs 2q, 2q + 1 of the step pair: 0..NP-1 -> step A, NP.. -> B
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int gp = 2 * q + e;
+      const double u = e ? z2 : z0, v = e ? z3 : z1;
+      if (gp < NP) { ra[2 * gp] = u; ra[2 * gp + 1] = v; }
+      else { rb[2 * (gp - NP)] = u; rb[2 * (gp - NP) + 1] = v; }
     }
   }
-  if (P % 2 == 0) {
-    const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
-    t0 = w.x;
-    t1 = w.y;
+  const u32x4 w = philox4x32_10(ctr(NP + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+  if constexpr (H % 2 == 1) {
+    ra[H - 1] = fast_normal_single(w.x, w.y, ta);
+    rb[H - 1] = fast_normal_single(w.z, w.w, tb);
+  } else {
+    ta = w.x >> 8;
+    tb = w.y >> 8;
   }
 }
 
@@ -557,6 +561,7 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   constexpr int H = D / 2;
   constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   constexpr bool REPLAY = RNG == PBH_RNG_REPLAY;
+  constexpr int LB = (H % 2 == 1) ? 14 : 24;   // Philox threshold lead bits
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   const int lane = threadIdx.x & 63;
   const bool hi = lane >= 32;
@@ -609,9 +614,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
 
   // One chain-step.  (r, t0, t1) are this step's draws (production Philox:
-  // drawn one step ahead); (rn, n0, n1) receive the next step's.
-  auto step = [&](int s, double (&r)[H], uint32_t &t0, uint32_t &t1,
-                  double (&rn)[H], uint32_t &n0, uint32_t &n1) {
+  // supplied by the caller, t0 = the LB-bit threshold lead).
+  auto step = [&](int s, double (&r)[H], uint32_t &t0, uint32_t &t1) {
     const int64_t g = a.g0 + s;
     double thr = 0.;
     if (REPLAY) {
@@ -633,9 +637,7 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       t0 = xo_next(xs);
       t1 = xo_next(xs);
     } else if (RNG == PBH_RNG_PHILOX) {
-      // software-pipelined: issue the next step's Philox blocks now so they
-      // overlap this step's fp64 chain (the draws never depend on state)
-      pair_draw_philox<H>(a, h, g + 1, chain, rn, n0, n1);
+      // drawn by the caller, a step pair ahead (pair2_draw_philox)
     } else {   // PHILOX_F64: fp64 Box-Muller
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
@@ -690,11 +692,24 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       q = q < 1. ? q : 1.;
       acc = first || q >= thr;
     } else {
-      const Decision dc = accept_filter(lpp, lp, t0, lin);
+      const Decision dc = RNG == PBH_RNG_PHILOX
+                              ? accept_filter_lead<LB>(lpp, lp, t0, lin)
+                              : accept_filter(lpp, lp, t0, lin);
       acc = first || dc.acc;
       const bool need = hi && !first && dc.need;
       if (__ballot(need)) {   // wave-uniform, rare
-        if (need) acc = ratio_accept(lpp, lp, u01(t0, t1), lin, a.log_npi);
+        if (need) {
+          double t;
+          if (RNG == PBH_RNG_PHILOX) {
+            // t's remaining 53 - LB bits from a block of this step alone
+            const u32x4 w = philox4x32_10(ctr(0x40u + 16u * h, g, chain),
+                                          a.seed_lo, a.seed_hi);
+            t = u01((t0 << (32 - LB)) | (w.x >> LB), w.y);
+          } else {
+            t = u01(t0, t1);
+          }
+          acc = ratio_accept(lpp, lp, t, lin, a.log_npi);
+        }
       }
     }
     // half 1's decision is the chain's: lanes l and l + 32 both take bit
@@ -729,15 +744,42 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     }
   };
 
-  double rA[H], rB[H];
-  uint32_t tA0 = 0, tA1 = 0, tB0 = 0, tB1 = 0;
-  if (RNG == PBH_RNG_PHILOX) pair_draw_philox<H>(a, h, a.g0, chain, rA, tA0, tA1);
-  int s = 0;
-  for (; s + 1 < a.n_steps; s += 2) {   // ping-pong the pipelined draws
-    step(s, rA, tA0, tA1, rB, tB0, tB1);
-    step(s + 1, rB, tB0, tB1, rA, tA0, tA1);
+  if constexpr (RNG == PBH_RNG_PHILOX) {
+    // Draws come per step PAIR (2P, 2P + 1), P = absolute step / 2, so a run
+    // split into launches at any step sees the same stream.  The next pair's
+    // blocks are issued while the current pair's fp64 chain runs (the draws
+    // never depend on state): ping-pong over two draw sets.
+    double cA[H], cB[H], nA[H], nB[H];
+    uint32_t ctA = 0, ctB = 0, ntA = 0, ntB = 0, t1 = 0;
+    int s = 0;
+    pair2_draw_philox<H>(a, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
+    if ((a.g0 & 1) && s < a.n_steps) {   // launch starts on a pair's 2nd step
+      step(s, cB, ctB, t1);
+      ++s;
+      if (s < a.n_steps)
+        pair2_draw_philox<H>(a, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+    }
+    for (; s + 3 < a.n_steps; s += 4) {
+      pair2_draw_philox<H>(a, h, ((a.g0 + s) >> 1) + 1, chain, nA, nB, ntA, ntB);
+      step(s, cA, ctA, t1);
+      step(s + 1, cB, ctB, t1);
+      pair2_draw_philox<H>(a, h, ((a.g0 + s) >> 1) + 2, chain, cA, cB, ctA, ctB);
+      step(s + 2, nA, ntA, t1);
+      step(s + 3, nB, ntB, t1);
+    }
+    if (s + 1 < a.n_steps) {
+      step(s, cA, ctA, t1);
+      step(s + 1, cB, ctB, t1);
+      s += 2;
+      if (s < a.n_steps)
+        pair2_draw_philox<H>(a, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+    }
+    if (s < a.n_steps) step(s, cA, ctA, t1);
+  } else {
+    double r[H];
+    uint32_t t0 = 0, t1 = 0;
+    for (int s = 0; s < a.n_steps; ++s) step(s, r, t0, t1);
   }
-  if (s < a.n_steps) step(s, rA, tA0, tA1, rB, tB0, tB1);
 
   if (active) {
 #pragma unroll
@@ -924,6 +966,369 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Production CondCov Gibbs kernel (PBH_RNG_PHILOX).  The replay kernel above
+// restates cond_cov.py:42-65 operation by operation; this one samples the
+// same conditional law at a fraction of the cost:
+//
+//  * one chain per group of L lanes (rows of 64/L lanes, L = 4 at d % 4 == 0),
+//    so 32 768 chains fill 2 048 wavefronts (2 per SIMD) instead of 512.
+//    Every lane of a group holds the chain's full state; the groups' lanes
+//    split the normal draws, the running moments and the trace stores.
+//  * x_k ~ N(m_k, sd_k) truncated to the reference's cdf limits
+//    (cond_cov.py:57-62: ppf(U(cdf_lo, cdf_hi)) is exactly the standard
+//    normal truncated to [ndtri(cdf_lo), ndtri(cdf_hi)]): an fp64 Box-Muller
+//    normal, replaced -- under a wave-uniform branch, for the lanes that need
+//    it -- by the reference's inversion draw when it falls outside those
+//    limits.  That mixture is exactly the truncated normal.  Each lane makes
+//    one Box-Muller pair per coordinate cycle and the group all-gathers the
+//    cycle's d normals through v_permlane16/32_swap.
+//  * v.prob: the quadratic form Q = (x[perm] - mu)^T Sigma^-1 (x[perm] - mu)
+//    (prob.py:349-358, App. A-4) is kept up to date in O(d) per coordinate
+//    update: with g = P'(x - mu') (P', mu' the precision and mean re-indexed
+//    to x order), a change D of x_k gives Q += D (g_k + g'_k), g += D P'_k.
+//    g and Q are recomputed exactly every kRefreshCycles coordinate cycles
+//    (absolute cycle index) and persisted between launches, so results do not depend on how
+//    a run is split into launches.  An fp64 GEMV per coordinate step -- the
+//    VALU or MFMA form -- costs d^2 instead of d: on gfx950 the fp64 matrix
+//    rate equals the fp64 vector rate, so the matrix cores buy nothing here
+//    (DESIGN.md §4).
+// ---------------------------------------------------------------------------
+constexpr int kRefreshCycles = 32;   // g, Q refreshed every 32 coordinate cycles
+
+// v_permlane32_swap with both operands = v: lo = the value of lane l & 31,
+// hi = the value of lane l | 32, in every lane.
+__device__ __forceinline__ void halves_f64(double v, double &lo, double &hi) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  lo = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
+  hi = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
+}
+
+// v_permlane16_swap with both operands = v: ev / od = the value of this
+// lane's position in the even / odd 16-lane row of its row pair.
+__device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  ev = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
+  od = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
+}
+
+// all[q * M + i] = own[i] of the group's lane in part q (part = row index).
+template <int L, int M>
+__device__ __forceinline__ void gather_parts(const double (&own)[M],
+                                             double (&all)[L * M]) {
+  if constexpr (L == 1) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) all[i] = own[i];
+  } else if constexpr (L == 2) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) halves_f64(own[i], all[i], all[M + i]);
+  } else {
+    static_assert(L == 4, "lanes per chain: 1, 2 or 4");
+    double blk[2 * M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) rowpair_f64(own[i], blk[i], blk[M + i]);
+#pragma unroll
+    for (int j = 0; j < 2 * M; ++j) halves_f64(blk[j], all[j], all[2 * M + j]);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ double part_sum(double v) {
+  // sum of v over the L lanes of a group, identical (same order) in each
+  if constexpr (L == 1) {
+    return v;
+  } else if constexpr (L == 2) {
+    double lo, hi;
+    halves_f64(v, lo, hi);
+    return lo + hi;
+  } else {
+    double ev, od, lo, hi;
+    rowpair_f64(v, ev, od);
+    halves_f64(ev + od, lo, hi);
+    return lo + hi;
+  }
+}
+
+template <int L, int Q>
+__device__ __forceinline__ double part_bcast(double v) {
+  // the value of part Q's lane of the group, in every lane of it
+  if constexpr (L == 1) {
+    return v;
+  } else if constexpr (L == 2) {
+    double lo, hi;
+    halves_f64(v, lo, hi);
+    return Q ? hi : lo;
+  } else {
+    double ev, od, lo, hi;
+    rowpair_f64(v, ev, od);
+    halves_f64((Q & 1) ? od : ev, lo, hi);
+    return (Q >> 1) ? hi : lo;
+  }
+}
+
+template <int D, int L>
+struct GibbsFast {
+  static constexpr int M = D / L;     // dims owned per lane
+  static constexpr int CW = 64 / L;   // chains per wavefront
+  // per-lane constants of the owned dims i = p M + ii, for every coordinate K:
+  // cf[K][ii] = coef_K at dim i (0 for i == K); pp[K][ii] = P'[K][i]
+  double cf[D][M], pp[D][M];
+  // per-coordinate constants (identical in every lane, held in VGPRs so the
+  // step loop issues no scalar loads): a_K, sd_K, P'_KK
+  double ak[D], sd[D], pkk[D];
+  double x[D];      // the state, every dim (identical in the group)
+  double z[D];      // this coordinate cycle's normals (identical)
+  double xo[M];     // owned dims of x
+  double go[M];     // owned dims of g = P'(x - mu')
+  double ms[M], mq[M];   // running moments of the owned dims
+  double Q;         // (x - mu')^T g (identical)
+  double lp;        // v.prob of the state
+  int p;            // part = lane / CW
+
+  __device__ __forceinline__ void load_consts(const KArgs &a) {
+#pragma unroll
+    for (int K = 0; K < D; ++K) {
+#pragma unroll
+      for (int ii = 0; ii < M; ++ii) {
+        const int i = p * M + ii;
+        cf[K][ii] = i == K ? 0. : a.gcoef[K * (D - 1) + (i < K ? i : i - 1)];
+        pp[K][ii] = a.gpp[K * D + i];
+      }
+      ak[K] = cld(a.gak, K);
+      sd[K] = cld(a.gstdv, K);
+      pkk[K] = cld(a.gpp, K * D + K);
+    }
+  }
+
+  // g = P'(x - mu') on the owned dims, Q = (x - mu')^T g  (exact refresh)
+  __device__ __forceinline__ void refresh(const KArgs &a) {
+    double dp[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) dp[j] = x[j] - cld(a.gmup, j);
+    double q = 0.;
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) {
+      double s = 0.;
+#pragma unroll
+      for (int j = 0; j < D; ++j) s = __builtin_fma(pp[j][ii], dp[j], s);  // P' symmetric
+      go[ii] = s;
+      double dpi = 0.;
+#pragma unroll
+      for (int q2 = 0; q2 < L; ++q2)
+        if (q2 == p) dpi = dp[q2 * M + ii];
+      q = __builtin_fma(dpi, s, q);
+    }
+    Q = part_sum<L>(q);
+  }
+
+  // The d normals of the coordinate cycle starting at step gc: part q draws
+  // coordinates [q M, q M + M) from Philox blocks 0x100 + 16 q + b.
+  __device__ __forceinline__ void draw_cycle(const KArgs &a, int64_t gc,
+                                             int64_t chain) {
+    double own[M];
+#pragma unroll
+    for (int b = 0; b < (M + 1) / 2; ++b) {
+      double z0, z1;
+      box_muller(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain), a.seed_lo,
+                               a.seed_hi), z0, z1);
+      own[2 * b] = z0;
+      if (2 * b + 1 < M) own[2 * b + 1] = z1;
+    }
+    gather_parts<L, M>(own, z);
+    // Truncation (cond_cov.py:57-62): a normal outside coordinate k's limits
+    // is replaced by the reference's inversion draw ppf(U(cdf_lo, cdf_hi)).
+    // Rare; one wave-uniform loop keeps a single copy of ndtri in the code.
+    uint32_t badm = 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      badm |= (z[k] >= cld(a.gzlo, k) && z[k] <= cld(a.gzhi, k)) ? 0u : (1u << k);
+    while (__ballot(badm != 0)) {
+      const int k = badm ? __builtin_ctz(badm) : 0;
+      double lo = 0., hi = 1.;
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk)
+        if (kk == k) { lo = cld(a.gcdf, 2 * kk); hi = cld(a.gcdf, 2 * kk + 1); }
+      const u32x4 w = philox4x32_10(ctr(0x200u + k, gc, chain), a.seed_lo, a.seed_hi);
+      const double zr = ndtri(lo + (hi - lo) * u01(w.x, w.y));
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk)
+        if (badm != 0 && kk == k) z[kk] = zr;
+      badm &= badm - 1;
+    }
+  }
+
+  // One coordinate update of coordinate K (cond_cov.py:42-65):
+  // x_K = mean_K + coef_K . (x_-K - mean_-K) + sd_K z_K
+  //     = a_K + coef_K . x_-K + sd_K z_K,  a_K = mean_K - coef_K . mean_-K,
+  // then the O(1)-per-lane update of g and Q.  The state is x itself, so a
+  // run split into launches reloads exactly the values it stored.
+  template <int K>
+  __device__ __forceinline__ void update() {
+    constexpr int OQ = K / M, OI = K % M;   // owning part, its local index
+    double d0 = 0., d1 = 0.;
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) {
+      if (ii & 1) d1 = __builtin_fma(cf[K][ii], xo[ii], d1);
+      else d0 = __builtin_fma(cf[K][ii], xo[ii], d0);
+    }
+    const double dot = part_sum<L>(d0 + d1) + ak[K];
+    const double xn = __builtin_fma(z[K], sd[K], dot);
+    const double del = xn - x[K];
+    x[K] = xn;
+    if (p == OQ) xo[OI] = xn;
+    const double gk = part_bcast<L, OQ>(go[OI]);
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) go[ii] = __builtin_fma(pp[K][ii], del, go[ii]);
+    const double gkn = __builtin_fma(pkk[K], del, gk);
+    Q = __builtin_fma(del, gk + gkn, Q);
+  }
+};
+
+// Per-launch state and step epilogue of gibbs_fast_kernel.  Everything the
+// step loop touches is a member (no lambdas capturing by reference), so the
+// whole state is promoted to registers.
+template <int D, int L>
+struct GibbsFastRun : GibbsFast<D, L> {
+  using B = GibbsFast<D, L>;
+  static constexpr int M = B::M, CW = B::CW;
+  int64_t c, wave, ri;
+  int lane, ph;
+  bool active, lin;
+  uint64_t act;
+
+  // after a step: v.prob, moments, trace record
+  __device__ __forceinline__ void post(const KArgs &a) {
+    const double lq = -0.5 * (a.gconst + this->Q);
+    this->lp = lin ? fast_exp(lq) : lq;
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) {
+      this->ms[ii] += this->xo[ii];
+      this->mq[ii] = __builtin_fma(this->xo[ii], this->xo[ii], this->mq[ii]);
+    }
+    const bool rec_now = ph == 0;
+    const int64_t rec = ri;
+    ph = (ph + 1 == a.thin) ? 0 : ph + 1;
+    ri += (ph == 0) ? 1 : 0;
+    if (rec_now && rec >= 0 && rec < a.rec_cap) {
+      if (active) {
+#pragma unroll
+        for (int ii = 0; ii < M; ++ii)
+          a.tx[(rec * D + this->p * M + ii) * a.n + c] = this->xo[ii];
+        if (this->p == 0) a.tlp[rec * a.n + c] = this->lp;
+      }
+      // u is always True for Gibbs (sp_utils.py:75-84): the active chains
+      if (lane == 0 && wave < (64 / CW) * a.W) {   // stay inside the record
+        const int64_t wi = rec * (64 / CW) * a.W + wave;
+        if constexpr (CW == 64) a.tacc[wi] = act;
+        else if constexpr (CW == 32) reinterpret_cast<uint32_t *>(a.tacc)[wi] = (uint32_t)act;
+        else reinterpret_cast<uint16_t *>(a.tacc)[wi] = (uint16_t)act;
+      }
+    }
+  }
+
+  // Coordinates [kb, ke) of a cycle, unrolled at compile time (a runtime
+  // coordinate index would make the compiler merge the per-coordinate code
+  // and index the constant arrays dynamically, i.e. through scratch).  A
+  // step ends after coordinate K when bit K of post_mask is set.  FULL: the
+  // whole cycle of single-coordinate steps, with no predicates at all.
+  template <bool FULL, int... K>
+  __device__ __forceinline__ void cycle(const KArgs &a, int kb, int ke,
+                                        uint32_t post_mask,
+                                        std::integer_sequence<int, K...>) {
+    if constexpr (FULL) {
+      ((this->template update<K>(), post(a)), ...);
+    } else {
+      ((K >= kb && K < ke
+            ? (this->template update<K>(),
+               ((post_mask >> K) & 1u) ? post(a) : void())
+            : void()),
+       ...);
+    }
+  }
+};
+
+template <int D, int L>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L == 4 && D <= 8 ? 2 : 1)))
+void gibbs_fast_kernel(KArgs a) {
+  using S = GibbsFastRun<D, L>;
+  constexpr int M = S::M, CW = S::CW;
+  S st;
+  st.lane = threadIdx.x & 63;
+  st.wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  st.c = st.wave * CW + (st.lane % CW);
+  st.active = st.c < a.n;
+  const int64_t cc = st.active ? st.c : 0;
+  const int64_t chain = a.off + cc;
+  st.lin = a.pscale == PBH_PSCALE_LIN;
+  st.p = st.lane / CW;
+  const int p = st.p;
+  st.load_consts(a);
+#pragma unroll
+  for (int k = 0; k < D; ++k) st.x[k] = a.x[k * a.n + cc];
+#pragma unroll
+  for (int ii = 0; ii < M; ++ii) {
+    st.xo[ii] = a.x[(p * M + ii) * a.n + cc];
+    st.ms[ii] = st.mq[ii] = 0.;
+  }
+  if (a.gq_init) {
+    st.refresh(a);
+  } else {
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) st.go[ii] = a.gq[(p * M + ii) * a.n + cc];
+    st.Q = a.gq[D * a.n + cc];
+  }
+  st.lp = a.lp[cc];
+  const int ts = a.tsteps;
+  const int nblk = (D + ts - 1) / ts;
+  int cm = (int)(a.g0 % nblk) * ts;    // first coordinate of the next step
+  st.draw_cycle(a, a.g0 - a.g0 % nblk, chain);
+  st.act = __ballot(st.active && p == 0);
+  st.ph = (int)((a.g0 + 1) % a.thin);
+  st.ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  int64_t cyc = (a.g0 + nblk - 1) / nblk;   // index of the next cycle start
+
+  // steps end after coordinates ts - 1, 2 ts - 1, ..., and d - 1
+  uint32_t post_mask = 1u << (D - 1);
+  for (int k = ts - 1; k < D; k += ts) post_mask |= 1u << k;
+  int s = 0;
+  bool entry = true;   // the entry drew the current cycle already
+  while (s < a.n_steps) {
+    if (cm == 0) {     // a coordinate cycle starts
+      if (!entry) st.draw_cycle(a, a.g0 + s, chain);
+      if ((cyc & (kRefreshCycles - 1)) == 0) st.refresh(a);
+      ++cyc;
+    }
+    entry = false;
+    const int nst = min(nblk - cm / ts, a.n_steps - s);   // steps in this cycle
+    const int ke = min(D, cm + nst * ts);
+    if (ts == 1 && cm == 0 && ke == D)
+      st.template cycle<true>(a, 0, D, post_mask, std::make_integer_sequence<int, D>{});
+    else
+      st.template cycle<false>(a, cm, ke, post_mask, std::make_integer_sequence<int, D>{});
+    s += nst;
+    cm = ke == D ? 0 : ke;
+  }
+  if (st.active) {
+    const int64_t c = st.c;
+#pragma unroll
+    for (int ii = 0; ii < M; ++ii) {
+      a.x[(p * M + ii) * a.n + c] = st.xo[ii];
+      a.msum[(p * M + ii) * a.n + c] += st.ms[ii];
+      a.msq[(p * M + ii) * a.n + c] += st.mq[ii];
+      a.gq[(p * M + ii) * a.n + c] = st.go[ii];
+    }
+    if (p == 0) {
+      a.lp[c] = st.lp;
+      a.nacc[c] += a.n_steps;
+      a.gq[D * a.n + c] = st.Q;
+    }
+  }
+}
+
 }  // namespace
 
 template <int D, int TGT, int PROP>
@@ -997,6 +1402,31 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
 
 template <int D>
 hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
+  if (gibbs_fast_form(a)) {
+    // lanes per chain: PBH_GIBBS_LANES if it divides d, else the default
+    // (2 for even d <= 12, measured fastest at d = 8; 4 for d = 16, whose
+    // per-lane constant block 2 d^2 / L would not fit the VGPRs at L = 2)
+    constexpr int LD = D % 2 ? 1 : (D <= 12 ? 2 : (D % 4 == 0 ? 4 : 2));
+    const int L = (a.gibbs_lanes > 0 && D % a.gibbs_lanes == 0 &&
+                   (a.gibbs_lanes == 1 || a.gibbs_lanes == 2 || a.gibbs_lanes == 4))
+                      ? a.gibbs_lanes : LD;
+    const int64_t waves = (a.n + 64 / L - 1) / (64 / L);
+    const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
+    if constexpr (D % 4 == 0) {
+      if (L == 4) {
+        hipLaunchKernelGGL((gibbs_fast_kernel<D, 4>), grid, block, 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    if constexpr (D % 2 == 0) {
+      if (L == 2) {
+        hipLaunchKernelGGL((gibbs_fast_kernel<D, 2>), grid, block, 0, st, a);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((gibbs_fast_kernel<D, 1>), grid, block, 0, st, a);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
   if constexpr (D <= 16) {
     if (a.gibbs_mfma) {

@@ -58,17 +58,29 @@ def run(name, n, steps, rng='philox', spl=0, trace=True):
 
 
 def main():
+  import argparse
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--only', default='cfg1,cfg3,cfg5',
+                  help='comma-separated subset of cfg1,cfg3,cfg5')
+  only = ap.parse_args().only.split(',')
   lines = []
-  eng, o = run('metrohast_norm1d', 128, 2000)
-  eng.close()
-  lines.append(dict(o, config='cfg1 (128 chains)'))
-  eng, o = run('metrohast_norm1d', 65536, 1000)
-  eng.close()
-  lines.append(dict(o, config='cfg1 model at 65536 chains'))
-  eng, o = run('gibbs8', 32768, 8 * 256)
-  o['coordinate_steps_per_s'] = o.pop('chain_steps_per_s')
-  eng.close()
-  lines.append(dict(o, config='cfg3'))
+  if 'cfg1' in only:
+    eng, o = run('metrohast_norm1d', 128, 2000)
+    eng.close()
+    lines.append(dict(o, config='cfg1 (128 chains)'))
+    eng, o = run('metrohast_norm1d', 65536, 1000)
+    eng.close()
+    lines.append(dict(o, config='cfg1 model at 65536 chains'))
+  if 'cfg3' in only:
+    eng, o = run('gibbs8', 32768, 8 * 256)
+    o['coordinate_steps_per_s'] = o.pop('chain_steps_per_s')
+    o['hbm_gbs'] = o['coordinate_steps_per_s'] * (8 * 8 + 8 + 1 / 8) / 1e9
+    eng.close()
+    lines.append(dict(o, config='cfg3'))
+  if 'cfg5' not in only:
+    for line in lines:
+      print(json.dumps(line), flush=True)
+    return
   eng, o = run('gmm2', 32768, 2000)
   t0 = time.perf_counter()
   tr = eng.trace()
