@@ -269,6 +269,17 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
     }
     ow = pack(blk, w.data(), d);
   }
+  if (m->target_kind == PBH_TARGET_GMM) {
+    // Production path: w_k = sqrt(0.5) / sd_k, c_k = logw_k - d (logC +
+    // log sd_k), so a_k = c_k - sum_i ((x_i - mu_ki) w_k)^2.
+    const double logC = std::log(std::sqrt(2 * M_PI));
+    std::vector<double> wc(2 * m->n);
+    for (int64_t k = 0; k < m->n; ++k) {
+      wc[k] = std::sqrt(0.5) / C[k];
+      wc[m->n + k] = A[k] - d * (logC + E[k]);
+    }
+    ow = pack(blk, wc.data(), 2 * m->n);
+  }
   if (m->target_kind == PBH_TARGET_NORM_IID) {
     // Production path: centred sufficient statistics of the observations,
     // sum_j (obs_j - mu)^2 = S2 + n (obar - mu)^2 -> O(1) per chain-step.
@@ -650,6 +661,9 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     const double qt = k.pscale == PBH_PSCALE_LIN
                           ? v : (v <= k.log_npi ? std::exp(v) : 1.7976931348623158e+308);
     k.pair_ok = (e->pair_enabled && (k.scores == PBH_SCORES_METROPOLIS || qt > 0.0)) ? 1 : 0;
+    k.simple_acc = (k.scores == PBH_SCORES_METROPOLIS ||
+                    (k.scores == PBH_SCORES_HASTINGS && k.tran_sym &&
+                     k.tran_kind == PBH_TRAN_CONST && qt > 0.0)) ? 1 : 0;
   }
   k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
   k.gibbs_fast = e->gibbs_fast ? 1 : 0;

@@ -161,6 +161,28 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
     case PBH_TARGET_GMM: {
       // a_k = logw_k + sum_i logpdf(x_i, mu_ki, sd_k); m + log(sum exp(a - m))
       const int64_t K = a.tn;
+      if (FAST) {
+        // production path: a_k = c_k - sum_i ((x_i - mu_ki) w_k)^2 with
+        // w_k = sqrt(.5) / sd_k, c_k = logw_k - d (logC + log sd_k) (host);
+        // two passes (max, then sum of exp) recompute the cheap a_k rather
+        // than keep K values in registers
+        auto comp = [&](int64_t k) {
+          const double w = cld(a.tw, k);
+          double v = cld(a.tw, K + k);
+#pragma unroll
+          for (int i = 0; i < D; ++i) {
+            const double u = (x[i] - cld(a.tb, k * D + i)) * w;
+            v = __builtin_fma(-u, u, v);
+          }
+          return v;
+        };
+        double m = comp(0);
+        for (int64_t k = 1; k < K; ++k) m = __builtin_fmax(m, comp(k));
+        double sum = 0.;
+        for (int64_t k = 0; k < K; ++k) sum += fast_exp(comp(k) - m);
+        out = m + log(sum);
+        break;
+      }
       auto comp = [&](int64_t k) {
         double v = cld(a.ta, k);
 #pragma unroll
@@ -282,6 +304,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   const int prop = PROP ? PROP : a.prop;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
+  // production modes with the symmetric ratio form: the acceptance filter
+  const bool simple = FAST && a.simple_acc && !a.debug;
   extern __shared__ double s_obs[];
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = c < a.n;
@@ -321,6 +345,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     // ---- draws ----
     double r[D];
     double thr;
+    uint32_t tw0 = 0, tw1 = 0;   // threshold words: thr = u01(tw0, tw1)
     if (RNG == PBH_RNG_REPLAY) {
       const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
 #pragma unroll
@@ -344,8 +369,9 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
           r[k] = u01(w0, xo_next(xs));
         }
       }
-      const uint32_t t0 = xo_next(xs);
-      thr = u01(t0, xo_next(xs));
+      tw0 = xo_next(xs);
+      tw1 = xo_next(xs);
+      thr = u01(tw0, tw1);
     } else if (FAST && prop == PBH_PROP_GAUSS) {
       // two normal pairs per Philox block; an odd pair count leaves the
       // block's second half for the 53-bit threshold
@@ -363,11 +389,15 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
           if (4 * q + 2 < D) r[4 * q + 2] = z2;
           if (4 * q + 3 < D) r[4 * q + 3] = z3;
         } else {
+          tw0 = w.y;
+          tw1 = w.w;
           thr = u01(w.y, w.w);
         }
       }
       if (P % 2 == 0) {
         const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+        tw0 = w.x;
+        tw1 = w.y;
         thr = u01(w.x, w.y);
       }
     } else {
@@ -388,6 +418,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         }
       }
       const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+      tw0 = w.x;
+      tw1 = w.y;
       thr = u01(w.x, w.y);
     }
     // ---- proposal ----
@@ -425,13 +457,23 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     }
     // ---- density, score, accept ----
     const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
-    const double eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
-                                        : exp_logp(lpp, a.log_npi));
+    double eA = 0.;
     double sc = __builtin_nan("");
     bool acc;
     if (!a.has_pred && s == 0) {
       acc = true;                                  // s = None on step 1
+      if (!simple) eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
+                                          : exp_logp(lpp, a.log_npi));
+    } else if (simple) {
+      // the ratio form's decision through the filter (see mh_pair_kernel)
+      const Decision dc = accept_filter(lpp, lp, tw0, lin);
+      acc = dc.acc;
+      if (__ballot(dc.need)) {   // wave-uniform, rare
+        if (dc.need) acc = ratio_accept(lpp, lp, u01(tw0, tw1), lin, a.log_npi);
+      }
     } else {
+      eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
+                             : exp_logp(lpp, a.log_npi));
       acc = !score<D>(a, x, xp, lp, lpp, eA, eB, sc) || (sc >= thr);
     }
     if (acc) {
