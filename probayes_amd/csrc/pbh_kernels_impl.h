@@ -776,8 +776,8 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       double *row = a.tx + rec * D * a.n;
       if (active) {
 #pragma unroll
-        for (int i = 0; i < H; ++i) row[(k0 + i) * a.n + c] = x[i];
-        if (hi) a.tlp[rec * a.n + c] = lp;
+        for (int i = 0; i < H; ++i) __builtin_nontemporal_store(x[i], &row[(k0 + i) * a.n + c]);
+        if (hi) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
       }
       // 32 chains per wave: the upper half's ballot bits are the mask word
       if (lane == 32 && (c >> 5) < 2 * a.W)
