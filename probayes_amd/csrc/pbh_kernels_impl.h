@@ -1116,41 +1116,42 @@ template <int D, int L>
 struct GibbsFast {
   static constexpr int M = D / L;     // dims owned per lane
   static constexpr int CW = 64 / L;   // chains per wavefront
-  // per-lane constants of the owned dims i = p M + ii, for every coordinate K:
-  // cf[K][ii] = coef_K at dim i (0 for i == K); pp[K][ii] = P'[K][i]
+  // Per-lane constants of the owned dims i = p M + ii.  For every coordinate
+  // K: cf[K][ii] = coef_K at dim i (0 for i == K), pp[K][ii] = P'[K][i];
+  // for the owned coordinates: ako[ii] = a_i, sdo[ii] = sd_i.
   double cf[D][M], pp[D][M];
-  // per-coordinate constants (identical in every lane, held in VGPRs so the
-  // step loop issues no scalar loads): a_K, sd_K, P'_KK
-  double ak[D], sd[D], pkk[D];
-  double x[D];      // the state, every dim (identical in the group)
-  double z[D];      // this coordinate cycle's normals (identical)
-  double xo[M];     // owned dims of x
+  double ako[M], sdo[M];
+  double zlo[M], zhi[M];   // truncation limits of the owned coordinates' z
+  double xo[M];     // owned dims of x (the state)
+  double zo[M];     // this cycle's normals of the owned coordinates
   double go[M];     // owned dims of g = P'(x - mu')
   double ms[M], mq[M];   // running moments of the owned dims
-  double Q;         // (x - mu')^T g (identical)
+  double Q;         // (x - mu')^T g (identical in the group)
   double lp;        // v.prob of the state
   int p;            // part = lane / CW
 
   __device__ __forceinline__ void load_consts(const KArgs &a) {
 #pragma unroll
-    for (int K = 0; K < D; ++K) {
+    for (int ii = 0; ii < M; ++ii) {
+      const int i = p * M + ii;
 #pragma unroll
-      for (int ii = 0; ii < M; ++ii) {
-        const int i = p * M + ii;
+      for (int K = 0; K < D; ++K) {
         cf[K][ii] = i == K ? 0. : a.gcoef[K * (D - 1) + (i < K ? i : i - 1)];
         pp[K][ii] = a.gpp[K * D + i];
       }
-      ak[K] = cld(a.gak, K);
-      sd[K] = cld(a.gstdv, K);
-      pkk[K] = cld(a.gpp, K * D + K);
+      ako[ii] = a.gak[i];
+      sdo[ii] = a.gstdv[i];
+      zlo[ii] = a.gzlo[i];
+      zhi[ii] = a.gzhi[i];
     }
   }
 
   // g = P'(x - mu') on the owned dims, Q = (x - mu')^T g  (exact refresh)
   __device__ __forceinline__ void refresh(const KArgs &a) {
-    double dp[D];
+    double dpo[M], dp[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) dp[j] = x[j] - cld(a.gmup, j);
+    for (int ii = 0; ii < M; ++ii) dpo[ii] = xo[ii] - a.gmup[p * M + ii];
+    gather_parts<L, M>(dpo, dp);
     double q = 0.;
 #pragma unroll
     for (int ii = 0; ii < M; ++ii) {
@@ -1158,56 +1159,51 @@ struct GibbsFast {
 #pragma unroll
       for (int j = 0; j < D; ++j) s = __builtin_fma(pp[j][ii], dp[j], s);  // P' symmetric
       go[ii] = s;
-      double dpi = 0.;
-#pragma unroll
-      for (int q2 = 0; q2 < L; ++q2)
-        if (q2 == p) dpi = dp[q2 * M + ii];
-      q = __builtin_fma(dpi, s, q);
+      q = __builtin_fma(dpo[ii], s, q);
     }
     Q = part_sum<L>(q);
   }
 
-  // The d normals of the coordinate cycle starting at step gc: part q draws
-  // coordinates [q M, q M + M) from Philox blocks 0x100 + 16 q + b.
+  // The normals of this lane's coordinates [p M, p M + M) for the coordinate
+  // cycle starting at step gc, from Philox blocks 0x100 + 16 p + b.
   __device__ __forceinline__ void draw_cycle(const KArgs &a, int64_t gc,
                                              int64_t chain) {
-    double own[M];
 #pragma unroll
     for (int b = 0; b < (M + 1) / 2; ++b) {
       double z0, z1;
       box_muller(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain), a.seed_lo,
                                a.seed_hi), z0, z1);
-      own[2 * b] = z0;
-      if (2 * b + 1 < M) own[2 * b + 1] = z1;
+      zo[2 * b] = z0;
+      if (2 * b + 1 < M) zo[2 * b + 1] = z1;
     }
-    gather_parts<L, M>(own, z);
     // Truncation (cond_cov.py:57-62): a normal outside coordinate k's limits
     // is replaced by the reference's inversion draw ppf(U(cdf_lo, cdf_hi)).
     // Rare; one wave-uniform loop keeps a single copy of ndtri in the code.
     uint32_t badm = 0;
 #pragma unroll
-    for (int k = 0; k < D; ++k)
-      badm |= (z[k] >= cld(a.gzlo, k) && z[k] <= cld(a.gzhi, k)) ? 0u : (1u << k);
+    for (int ii = 0; ii < M; ++ii)
+      badm |= (zo[ii] >= zlo[ii] && zo[ii] <= zhi[ii]) ? 0u : (1u << ii);
     while (__ballot(badm != 0)) {
-      const int k = badm ? __builtin_ctz(badm) : 0;
-      double lo = 0., hi = 1.;
-#pragma unroll
-      for (int kk = 0; kk < D; ++kk)
-        if (kk == k) { lo = cld(a.gcdf, 2 * kk); hi = cld(a.gcdf, 2 * kk + 1); }
+      const int ii = badm ? __builtin_ctz(badm) : 0;
+      const int k = p * M + ii;
+      const double lo = a.gcdf[2 * k], hi = a.gcdf[2 * k + 1];
       const u32x4 w = philox4x32_10(ctr(0x200u + k, gc, chain), a.seed_lo, a.seed_hi);
       const double zr = ndtri(lo + (hi - lo) * u01(w.x, w.y));
 #pragma unroll
-      for (int kk = 0; kk < D; ++kk)
-        if (badm != 0 && kk == k) z[kk] = zr;
+      for (int jj = 0; jj < M; ++jj)
+        if (badm != 0 && jj == ii) zo[jj] = zr;
       badm &= badm - 1;
     }
   }
 
   // One coordinate update of coordinate K (cond_cov.py:42-65):
   // x_K = mean_K + coef_K . (x_-K - mean_-K) + sd_K z_K
-  //     = a_K + coef_K . x_-K + sd_K z_K,  a_K = mean_K - coef_K . mean_-K,
-  // then the O(1)-per-lane update of g and Q.  The state is x itself, so a
-  // run split into launches reloads exactly the values it stored.
+  //     = a_K + coef_K . x_-K + sd_K z_K,  a_K = mean_K - coef_K . mean_-K.
+  // Every part forms its share of the dot product; the owning part OQ makes
+  // x_K, its change D and the change of Q, D (g_K + g'_K), and broadcasts
+  // D and the Q change; every part then updates its own dims of g += D P'_K.
+  // The state is x itself, so a run split into launches reloads exactly the
+  // values it stored.
   template <int K>
   __device__ __forceinline__ void update() {
     constexpr int OQ = K / M, OI = K % M;   // owning part, its local index
@@ -1217,16 +1213,15 @@ struct GibbsFast {
       if (ii & 1) d1 = __builtin_fma(cf[K][ii], xo[ii], d1);
       else d0 = __builtin_fma(cf[K][ii], xo[ii], d0);
     }
-    const double dot = part_sum<L>(d0 + d1) + ak[K];
-    const double xn = __builtin_fma(z[K], sd[K], dot);
-    const double del = xn - x[K];
-    x[K] = xn;
-    if (p == OQ) xo[OI] = xn;
-    const double gk = part_bcast<L, OQ>(go[OI]);
+    const double dot = part_sum<L>(d0 + d1);
+    // meaningful in the owning part only
+    const double xn = __builtin_fma(zo[OI], sdo[OI], dot + ako[OI]);
+    const double del = part_bcast<L, OQ>(xn - xo[OI]);
+    const double gk = go[OI];
 #pragma unroll
     for (int ii = 0; ii < M; ++ii) go[ii] = __builtin_fma(pp[K][ii], del, go[ii]);
-    const double gkn = __builtin_fma(pkk[K], del, gk);
-    Q = __builtin_fma(del, gk + gkn, Q);
+    Q += part_bcast<L, OQ>(del * (gk + go[OI]));
+    if (p == OQ) xo[OI] = xn;
   }
 };
 
@@ -1242,10 +1237,14 @@ struct GibbsFastRun : GibbsFast<D, L> {
   bool active, lin;
   uint64_t act;
 
-  // after a step: v.prob, moments, trace record
-  __device__ __forceinline__ void post(const KArgs &a) {
-    const double lq = -0.5 * (a.gconst + this->Q);
-    this->lp = lin ? fast_exp(lq) : lq;
+  __device__ __forceinline__ double vprob(const KArgs &a, double q) const {
+    const double lq = -0.5 * (a.gconst + q);
+    return lin ? fast_exp(lq) : lq;
+  }
+
+  // after a step: moments, trace record of x and u; returns the step's
+  // record index, or -1 when the step is not recorded
+  __device__ __forceinline__ int64_t post_x(const KArgs &a) {
 #pragma unroll
     for (int ii = 0; ii < M; ++ii) {
       this->ms[ii] += this->xo[ii];
@@ -1255,12 +1254,12 @@ struct GibbsFastRun : GibbsFast<D, L> {
     const int64_t rec = ri;
     ph = (ph + 1 == a.thin) ? 0 : ph + 1;
     ri += (ph == 0) ? 1 : 0;
-    if (rec_now && rec >= 0 && rec < a.rec_cap) {
+    const bool r = rec_now && rec >= 0 && rec < a.rec_cap;
+    if (r) {
       if (active) {
 #pragma unroll
         for (int ii = 0; ii < M; ++ii)
-          a.tx[(rec * D + this->p * M + ii) * a.n + c] = this->xo[ii];
-        if (this->p == 0) a.tlp[rec * a.n + c] = this->lp;
+          __builtin_nontemporal_store(this->xo[ii], &a.tx[(rec * D + this->p * M + ii) * a.n + c]);
       }
       // u is always True for Gibbs (sp_utils.py:75-84): the active chains
       if (lane == 0 && wave < (64 / CW) * a.W) {   // stay inside the record
@@ -1269,6 +1268,34 @@ struct GibbsFastRun : GibbsFast<D, L> {
         else if constexpr (CW == 32) reinterpret_cast<uint32_t *>(a.tacc)[wi] = (uint32_t)act;
         else reinterpret_cast<uint16_t *>(a.tacc)[wi] = (uint16_t)act;
       }
+    }
+    return r ? rec : -1;
+  }
+
+  // after a step: v.prob of the state (every lane), then post_x
+  __device__ __forceinline__ void post(const KArgs &a) {
+    this->lp = vprob(a, this->Q);
+    const int64_t rec = post_x(a);
+    if (rec >= 0 && active && this->p == 0)
+      __builtin_nontemporal_store(this->lp, &a.tlp[rec * a.n + c]);
+  }
+
+  // Steps K - 1, K (K odd) of a paired cycle: parts with p odd evaluate
+  // step K's v.prob, parts with p even step K - 1's, so each lane runs one
+  // exp per two steps; parts 0 and 1 store the two records.
+  template <int K>
+  __device__ __forceinline__ void post_pair(const KArgs &a, double &qprev,
+                                            int64_t &rprev) {
+    const int64_t r = post_x(a);
+    if constexpr (K % 2 == 0) {
+      qprev = this->Q;
+      rprev = r;
+    } else {
+      const bool odd = this->p & 1;
+      const double v = vprob(a, odd ? this->Q : qprev);
+      const int64_t rr = odd ? r : rprev;
+      if (rr >= 0 && active && this->p < 2)
+        __builtin_nontemporal_store(v, &a.tlp[rr * a.n + c]);
     }
   }
 
@@ -1282,7 +1309,13 @@ struct GibbsFastRun : GibbsFast<D, L> {
                                         uint32_t post_mask,
                                         std::integer_sequence<int, K...>) {
     if constexpr (FULL) {
-      ((this->template update<K>(), post(a)), ...);
+      if constexpr (L >= 2 && D % 2 == 0) {
+        double qprev = 0.;
+        int64_t rprev = -1;
+        ((this->template update<K>(), post_pair<K>(a, qprev, rprev)), ...);
+      } else {
+        ((this->template update<K>(), post(a)), ...);
+      }
     } else {
       ((K >= kb && K < ke
             ? (this->template update<K>(),
@@ -1309,8 +1342,6 @@ void gibbs_fast_kernel(KArgs a) {
   st.p = st.lane / CW;
   const int p = st.p;
   st.load_consts(a);
-#pragma unroll
-  for (int k = 0; k < D; ++k) st.x[k] = a.x[k * a.n + cc];
 #pragma unroll
   for (int ii = 0; ii < M; ++ii) {
     st.xo[ii] = a.x[(p * M + ii) * a.n + cc];
@@ -1354,6 +1385,7 @@ void gibbs_fast_kernel(KArgs a) {
     s += nst;
     cm = ke == D ? 0 : ke;
   }
+  st.lp = st.vprob(a, st.Q);   // (paired cycles leave it unset)
   if (st.active) {
     const int64_t c = st.c;
 #pragma unroll
