@@ -661,9 +661,13 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     const double qt = k.pscale == PBH_PSCALE_LIN
                           ? v : (v <= k.log_npi ? std::exp(v) : 1.7976931348623158e+308);
     k.pair_ok = (e->pair_enabled && (k.scores == PBH_SCORES_METROPOLIS || qt > 0.0)) ? 1 : 0;
+    // metropolis_scores / hastings_scores with a constant tran are the ratio
+    // form of (lp', lp) -- or, for a tuple tran, of (lp' q~, lp q~): the
+    // reverse value equals the forward one (rf.py:536), sp_utils.py:59-64.
     k.simple_acc = (k.scores == PBH_SCORES_METROPOLIS ||
-                    (k.scores == PBH_SCORES_HASTINGS && k.tran_sym &&
+                    (k.scores == PBH_SCORES_HASTINGS &&
                      k.tran_kind == PBH_TRAN_CONST && qt > 0.0)) ? 1 : 0;
+    k.acc_beta = (k.scores == PBH_SCORES_HASTINGS && !k.tran_sym) ? qt : 1.0;
   }
   k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
   k.gibbs_fast = e->gibbs_fast ? 1 : 0;

@@ -58,8 +58,9 @@ struct KArgs {
   int32_t debug;
   int64_t W;         // accept-mask words per recorded step = ceil(n / 64)
   int32_t pair_ok;   // engine allows the lane-pair kernel (see launch_mh_d)
-  int32_t simple_acc;  // acceptance is the symmetric ratio form (metropolis, or
-                       // hastings with a symmetric constant tran, q~ > 0)
+  int32_t simple_acc;  // acceptance is the ratio form of beta lp', beta lp
+                       // (metropolis, or hastings with a constant tran, q~ > 0)
+  double acc_beta;     // 1, or q~ for a constant tuple tran (App. A-1)
   int32_t gibbs_mfma;  // Gibbs density quadratic form on MFMA (d <= 16)
   // ---- production CondCov Gibbs (gibbs_fast_kernel) ----
   int32_t gibbs_fast;  // engine allows the production Gibbs kernel

@@ -107,6 +107,31 @@ __device__ __forceinline__ double mvn_density(const KArgs &a,
   return a.pscale == PBH_PSCALE_LIN ? exp(logpdf) : logpdf;
 }
 
+// Production GMM log-density for a compile-time component count: the K
+// independent exp chains interleave (ILP at one wavefront per SIMD).
+template <int D, int K>
+__device__ __forceinline__ double gmm_fast(const KArgs &a, const double (&x)[D]) {
+  double v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double w = cld(a.tw, k);
+    double acc = cld(a.tw, K + k);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const double u = (x[i] - cld(a.tb, k * D + i)) * w;
+      acc = __builtin_fma(-u, u, acc);
+    }
+    v[k] = acc;
+  }
+  double m = v[0];
+#pragma unroll
+  for (int k = 1; k < K; ++k) m = __builtin_fmax(m, v[k]);
+  double sum = 0.;
+#pragma unroll
+  for (int k = 0; k < K; ++k) sum += fast_exp(v[k] - m);
+  return m + log(sum);
+}
+
 template <int D, int TGT, bool FAST>
 __device__ __forceinline__ double joint_density(const KArgs &a,
                                                 const double (&x)[D],
@@ -165,7 +190,10 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
         // production path: a_k = c_k - sum_i ((x_i - mu_ki) w_k)^2 with
         // w_k = sqrt(.5) / sd_k, c_k = logw_k - d (logC + log sd_k) (host);
         // two passes (max, then sum of exp) recompute the cheap a_k rather
-        // than keep K values in registers
+        // than keep K values in registers; K <= 4 unrolled at compile time
+        if (K == 3) { out = gmm_fast<D, 3>(a, x); break; }
+        if (K == 2) { out = gmm_fast<D, 2>(a, x); break; }
+        if (K == 4) { out = gmm_fast<D, 4>(a, x); break; }
         auto comp = [&](int64_t k) {
           const double w = cld(a.tw, k);
           double v = cld(a.tw, K + k);
@@ -465,11 +493,13 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       if (!simple) eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
                                           : exp_logp(lpp, a.log_npi));
     } else if (simple) {
-      // the ratio form's decision through the filter (see mh_pair_kernel)
-      const Decision dc = accept_filter(lpp, lp, tw0, lin);
+      // the ratio form's decision through the filter (see mh_pair_kernel);
+      // a constant tuple tran scales both log-probs by q~ (App. A-1)
+      const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
+      const Decision dc = accept_filter(bA, bB, tw0, lin);
       acc = dc.acc;
       if (__ballot(dc.need)) {   // wave-uniform, rare
-        if (dc.need) acc = ratio_accept(lpp, lp, u01(tw0, tw1), lin, a.log_npi);
+        if (dc.need) acc = ratio_accept(bA, bB, u01(tw0, tw1), lin, a.log_npi);
       }
     } else {
       eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)

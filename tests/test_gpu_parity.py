@@ -280,3 +280,28 @@ def test_iid_normal_pairwise_tree_matches_numpy(n_obs):
   assert np.array_equal(out['u'], ref['u'])
   assert _rel_err(out['p_p'], ref['p_p']) <= RTOL
   assert _rel_err(out['v_x'], ref['v_x'], 1.) <= RTOL
+
+
+@pytest.mark.parametrize('name', ['metrohast_norm1d', 'gmm2'])
+def test_production_modes_agree_with_reference_arithmetic(name):
+  """Production Philox (fast densities, filtered acceptance incl. the
+  e-tempered tuple-tran form of App. A-1) against PHILOX_F64 (fp64
+  Box-Muller, the reference's arithmetic): the same posterior within
+  Monte-Carlo error."""
+  spec = oracle.golden_spec(name)
+  n, t, burn = 4096, 800, 300
+  res = {}
+  for mode in ('philox', 'philox_f64'):
+    eng = _engine(spec)
+    eng.init_chains(golden_init(name, n))
+    eng.set_rng(mode, seed=77)
+    eng.alloc_trace(t, 1)
+    eng.run(t)
+    tr = eng.trace()
+    eng.close()
+    v = tr['v_x'][:, burn:]
+    res[mode] = (v.mean(axis=(0, 1)), v.std(axis=(0, 1)), tr['u'].mean())
+  (m1, s1, a1), (m0, s0, a0) = res['philox'], res['philox_f64']
+  assert np.all(np.abs(m1 - m0) < 0.05 * s0), (m1, m0, s0)
+  assert np.all(np.abs(s1 / s0 - 1) < 0.05), (s1, s0)
+  assert abs(a1 - a0) < 0.02, (a1, a0)
