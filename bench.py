@@ -83,13 +83,15 @@ def measured_traffic(chains, spl, rng, trace):
   None when no profile matches."""
   import glob
   files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic.json')))
-  if not files or not trace or rng != 'philox':
+  if not trace or rng != 'philox':
     return None
-  with open(files[-1]) as f:
-    t = json.load(f)
-  if t.get('chains') != chains or t.get('steps_per_launch') != spl:
-    return None
-  return t['bytes_per_launch']
+  for path in reversed(files):   # newest profile of this kernel and shape
+    with open(path) as f:
+      t = json.load(f)
+    if (t.get('kernel', '').startswith('mh_pair_kernel') and
+        t.get('chains') == chains and t.get('steps_per_launch') == spl):
+      return t['bytes_per_launch']
+  return None
 
 
 def main():
