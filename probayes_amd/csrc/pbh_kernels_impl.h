@@ -590,6 +590,27 @@ __device__ __forceinline__ double swap_f64(double v, bool hi) {
   return __builtin_bit_cast(double, lo | (up << 32));
 }
 
+// v_permlane32_swap with both operands = v: lo = the value of lane l & 31,
+// hi = the value of lane l | 32, in every lane.
+__device__ __forceinline__ void halves_f64(double v, double &lo, double &hi) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  lo = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
+  hi = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
+}
+
+// v_permlane16_swap with both operands = v: ev / od = the value of this
+// lane's position in the even / odd 16-lane row of its row pair.
+__device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  ev = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
+  od = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
+}
+
+
 // Production draws of a PAIR of half-steps (steps 2P, 2P + 1) of one lane:
 // NP = H / 2 Box-Muller pairs per step from NP Philox blocks (q < NP), and
 // one more block q = NP holding the odd normal of each step (H odd; its
@@ -869,6 +890,167 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Lane-pair MH kernel for the Gaussian-mixture target with the callable
+// Gaussian delta (cfg5, production RNG).  At d = 2 the one-chain-per-lane
+// kernel leaves every other SIMD idle at 32 768 chains; here one chain is a
+// lane PAIR (l, l + 32).  Both halves hold the whole state and draw the same
+// proposal (the same Philox block); the K components are split over the
+// halves (k = 2 kk + h), each half forms the log-sum-exp of its components,
+// and one exchange combines them: lse = M + log(s_M + s_m exp(m - M)).
+// Acceptance is the filtered ratio form, identical in both halves.
+// ---------------------------------------------------------------------------
+template <int D, int K>
+__global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
+  static_assert(K >= 2, "each half needs a component");
+  constexpr int KH = (K + 1) / 2;
+  constexpr double kNegInf = -__builtin_inf();
+  const bool lin = a.pscale == PBH_PSCALE_LIN;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >= 32 ? 1 : 0;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t c = wave * 32 + (lane & 31);
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const uint64_t act_mask = __ballot(active);
+  const int64_t chain = a.off + cc;
+
+  // this half's components k = 2 kk + h (a missing one contributes exp = 0)
+  double cw[KH], c0[KH], cmu[KH][D];
+#pragma unroll
+  for (int kk = 0; kk < KH; ++kk) {
+    const int k = 2 * kk + h;
+    const bool ok = k < K;
+    cw[kk] = ok ? a.tw[k] : 0.;
+    c0[kk] = ok ? a.tw[K + k] : kNegInf;
+#pragma unroll
+    for (int i = 0; i < D; ++i) cmu[kk][i] = ok ? a.tb[k * D + i] : 0.;
+  }
+  double x[D], ms[D], mq[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    x[i] = a.x[i * a.n + cc];
+    ms[i] = 0.;
+    mq[i] = 0.;
+  }
+  double lp = a.lp[cc];
+  int64_t nacc = 0;
+  int ph = (int)((a.g0 + 1) % a.thin);
+  int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const int64_t g = a.g0 + s;
+    // ---- draws: mh_kernel's production Gaussian path (same counters) ----
+    constexpr int P = (D + 1) / 2;
+    double r[D];
+    uint32_t tw0 = 0, tw1 = 0;
+#pragma unroll
+    for (int q = 0; q < (P + 1) / 2; ++q) {
+      const u32x4 w = philox4x32_10(ctr(q, g, chain), a.seed_lo, a.seed_hi);
+      double z1;
+      const double z0 = fast_normal_pair(w.x, w.z, z1);
+      if (4 * q < D) r[4 * q] = z0;
+      if (4 * q + 1 < D) r[4 * q + 1] = z1;
+      if (2 * q + 1 < P) {
+        double z3;
+        const double z2 = fast_normal_pair(w.y, w.w, z3);
+        if (4 * q + 2 < D) r[4 * q + 2] = z2;
+        if (4 * q + 3 < D) r[4 * q + 3] = z3;
+      } else {
+        tw0 = w.y;
+        tw1 = w.w;
+      }
+    }
+    if (P % 2 == 0) {
+      const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+      tw0 = w.x;
+      tw1 = w.y;
+    }
+    double xp[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      xp[i] = x[i] + __builtin_fma(r[i], cld(a.pscl, i), cld(a.ploc, i));
+    // ---- log-sum-exp over this half's components, then the pair's ----
+    double v[KH];
+#pragma unroll
+    for (int kk = 0; kk < KH; ++kk) {
+      double acc = c0[kk];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const double u = (xp[i] - cmu[kk][i]) * cw[kk];
+        acc = __builtin_fma(-u, u, acc);
+      }
+      v[kk] = acc;
+    }
+    double m = v[0];
+#pragma unroll
+    for (int kk = 1; kk < KH; ++kk) m = __builtin_fmax(m, v[kk]);
+    double sl = 0.;
+#pragma unroll
+    for (int kk = 0; kk < KH; ++kk) sl += fast_exp(v[kk] - m);
+    double m0, m1, s0, s1;
+    halves_f64(m, m0, m1);
+    halves_f64(sl, s0, s1);
+    const bool big0 = m0 >= m1;
+    const double e = fast_exp(-__builtin_fabs(m0 - m1));
+    const double S = big0 ? __builtin_fma(s1, e, s0) : __builtin_fma(s0, e, s1);
+    const double lpp = __builtin_fmax(m0, m1) + log(S);
+    // ---- acceptance (identical in both halves) ----
+    bool acc;
+    if (!a.has_pred && s == 0) {
+      acc = true;                                  // s = None on step 1
+    } else {
+      const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
+      const Decision dc = accept_filter(bA, bB, tw0, lin);
+      acc = dc.acc;
+      if (__ballot(dc.need)) {   // wave-uniform, rare
+        if (dc.need) acc = ratio_accept(bA, bB, u01(tw0, tw1), lin, a.log_npi);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
+    lp = acc ? lpp : lp;
+    nacc += acc ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      if (i % 2 == h) {
+        ms[i] += x[i];
+        mq[i] = __builtin_fma(x[i], x[i], mq[i]);
+      }
+    }
+    const bool rec_now = ph == 0;
+    const int64_t rec = ri;
+    ph = (ph + 1 == a.thin) ? 0 : ph + 1;
+    ri += (ph == 0) ? 1 : 0;
+    if (rec_now && rec >= 0 && rec < a.rec_cap) {
+      if (active) {
+        double *row = a.tx + rec * D * a.n;
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+          if (i % 2 == h) __builtin_nontemporal_store(x[i], &row[i * a.n + c]);
+        if (h == 0) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
+      }
+      const uint64_t am = __ballot(acc) & act_mask;   // halves agree
+      if (lane == 0 && wave < 2 * a.W)
+        reinterpret_cast<uint32_t *>(a.tacc)[rec * 2 * a.W + wave] = (uint32_t)am;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      if (i % 2 == h) {
+        a.x[i * a.n + c] = x[i];
+        a.msum[i * a.n + c] += ms[i];
+        a.msq[i * a.n + c] += mq[i];
+      }
+    }
+    if (h == 0) {
+      a.lp[c] = lp;
+      a.nacc[c] += nacc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // MFMA form of the mvn quadratic form for a wavefront of 64 chains:
 //   Y^T (16 x 16 chains) = U^T (16 x 4) . DEV^T (4 x 16 chains), K-chunks of 4
 // with v_mfma_f64_16x16x4_f64 (A = U^T, constant, in VGPRs; B = the chains'
@@ -1067,26 +1249,6 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
 //    (DESIGN.md §4).
 // ---------------------------------------------------------------------------
 constexpr int kRefreshCycles = 32;   // g, Q refreshed every 32 coordinate cycles
-
-// v_permlane32_swap with both operands = v: lo = the value of lane l & 31,
-// hi = the value of lane l | 32, in every lane.
-__device__ __forceinline__ void halves_f64(double v, double &lo, double &hi) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
-  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
-  lo = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
-  hi = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
-}
-
-// v_permlane16_swap with both operands = v: ev / od = the value of this
-// lane's position in the even / odd 16-lane row of its row pair.
-__device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
-  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
-  ev = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
-  od = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
-}
 
 // all[q * M + i] = own[i] of the group's lane in part q (part = row index).
 template <int L, int M>
@@ -1476,6 +1638,13 @@ inline bool pair_form(const KArgs &a) {
            a.tran_kind == PBH_TRAN_CONST));
 }
 
+// The GMM lane-pair kernel: production Philox, the filtered ratio form, no
+// ufun / prior / debug records.
+inline bool gmm_pair_form(const KArgs &a) {
+  return a.rng == PBH_RNG_PHILOX && a.simple_acc && a.pair_ok && a.ufun == 0 &&
+         !a.has_prior && !a.debug;
+}
+
 template <int D>
 hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
   if constexpr (D % 2 == 0 && D >= 4) {
@@ -1492,6 +1661,17 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
   }
   if constexpr (D <= 4) {
     if (a.target == PBH_TARGET_GMM && a.prop == PBH_PROP_GAUSS) {
+      if (gmm_pair_form(a) && a.tn >= 2 && a.tn <= 4) {
+        const int64_t waves = (a.n + 31) / 32;
+        const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
+        if (a.tn == 2)
+          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 2>), grid, block, 0, st, a);
+        else if (a.tn == 3)
+          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 3>), grid, block, 0, st, a);
+        else
+          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 4>), grid, block, 0, st, a);
+        return hipGetLastError();
+      }
       launch_mh_spec<D, PBH_TARGET_GMM, PBH_PROP_GAUSS>(a, st, lds);
       return hipGetLastError();
     }

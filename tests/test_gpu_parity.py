@@ -305,3 +305,29 @@ def test_production_modes_agree_with_reference_arithmetic(name):
   assert np.all(np.abs(m1 - m0) < 0.05 * s0), (m1, m0, s0)
   assert np.all(np.abs(s1 / s0 - 1) < 0.05), (s1, s0)
   assert abs(a1 - a0) < 0.02, (a1, a0)
+
+
+def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch):
+  """cfg5 form: the lane-pair GMM kernel (components split over the halves)
+  draws the same Philox stream as the one-chain-per-lane kernel; its
+  log-sum-exp differs only in rounding, so chains, accept bits and moments
+  agree and log-densities agree to ~1e-14 (ragged chain count)."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec('gmm2')
+  n, t = 3000, 300
+  outs = {}
+  for no_pair in ('0', '1'):
+    monkeypatch.setenv('PBH_NO_PAIR', no_pair)
+    eng = Engine(spec)
+    eng.init_chains(golden_init('gmm2', n))
+    eng.set_rng('philox', seed=5)
+    eng.alloc_trace(t, 1)
+    eng.run(t, steps_per_launch=128)
+    outs[no_pair] = (eng.trace(), eng.moments())
+    eng.close()
+  (tp, mp), (t1, m1) = outs['0'], outs['1']
+  assert np.array_equal(tp['u'], t1['u'])
+  np.testing.assert_allclose(tp['v_x'], t1['v_x'], rtol=0, atol=1e-12)
+  assert _rel_err(tp['v_p'], t1['v_p']) <= 1e-13
+  assert np.array_equal(mp['n_acc'], m1['n_acc'])
+  np.testing.assert_allclose(mp['sum'], m1['sum'], rtol=1e-12, atol=1e-9)
