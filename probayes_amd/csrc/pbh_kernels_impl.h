@@ -34,6 +34,15 @@ __device__ __forceinline__ double cld(const double *p, int64_t i) {
   return ((const __attribute__((address_space(4))) double *)p)[i];
 }
 
+// A wave-uniform value kept in SGPRs: a select between two such values
+// cannot then be turned into a vector load from a selected address.
+__device__ __forceinline__ double uni(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+
 // prob.py:354-357: the mvn density is evaluated at the values reversed and,
 // for d > 2, rotated by one: [x_{d-2}, ..., x_0, x_{d-1}] (App. A-4).
 template <int D>
@@ -1340,9 +1349,17 @@ struct GibbsFast {
 
   // g = P'(x - mu') on the owned dims, Q = (x - mu')^T g  (exact refresh)
   __device__ __forceinline__ void refresh(const KArgs &a) {
+    // No vector loads inside the step loop: a load's s_waitcnt vmcnt would
+    // also wait for every trace store issued before it.  mu' by scalar
+    // loads, selected per part.
     double dpo[M], dp[D];
 #pragma unroll
-    for (int ii = 0; ii < M; ++ii) dpo[ii] = xo[ii] - a.gmup[p * M + ii];
+    for (int ii = 0; ii < M; ++ii) {
+      double mu = uni(cld(a.gmup, ii));
+#pragma unroll
+      for (int q = 1; q < L; ++q) mu = p == q ? uni(cld(a.gmup, q * M + ii)) : mu;
+      dpo[ii] = xo[ii] - mu;
+    }
     gather_parts<L, M>(dpo, dp);
     double q = 0.;
 #pragma unroll
@@ -1378,7 +1395,10 @@ struct GibbsFast {
     while (__ballot(badm != 0)) {
       const int ii = badm ? __builtin_ctz(badm) : 0;
       const int k = p * M + ii;
-      const double lo = a.gcdf[2 * k], hi = a.gcdf[2 * k + 1];
+      double lo = 0., hi = 1.;   // scalar loads (see refresh)
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk)
+        if (kk == k) { lo = uni(cld(a.gcdf, 2 * kk)); hi = uni(cld(a.gcdf, 2 * kk + 1)); }
       const u32x4 w = philox4x32_10(ctr(0x200u + k, gc, chain), a.seed_lo, a.seed_hi);
       const double zr = ndtri(lo + (hi - lo) * u01(w.x, w.y));
 #pragma unroll
@@ -1559,6 +1579,9 @@ void gibbs_fast_kernel(KArgs a) {
   // steps end after coordinates ts - 1, 2 ts - 1, ..., and d - 1
   uint32_t post_mask = 1u << (D - 1);
   for (int k = ts - 1; k < D; k += ts) post_mask |= 1u << k;
+  // Drain the entry loads here: otherwise the waits for them land inside the
+  // loop, where each s_waitcnt vmcnt would also wait for the trace stores.
+  __builtin_amdgcn_s_waitcnt(0);
   int s = 0;
   bool entry = true;   // the entry drew the current cycle already
   while (s < a.n_steps) {
