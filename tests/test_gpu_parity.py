@@ -331,3 +331,32 @@ def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch):
   assert _rel_err(tp['v_p'], t1['v_p']) <= 1e-13
   assert np.array_equal(mp['n_acc'], m1['n_acc'])
   np.testing.assert_allclose(mp['sum'], m1['sum'], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize('name,thin,spl', [('diag10', 3, 0), ('diag10', 4, 7),
+                                           ('gmm2', 4, 9), ('gibbs8', 5, 13),
+                                           ('gibbs_sweep2', 3, 5)])
+def test_production_thinning_equals_every_kth_step(name, thin, spl):
+  """Production kernels (lane-pair MH, GMM lane-pair, Gibbs): a thinned
+  trace is exactly every thin-th record of the full trace, whatever the
+  launch split (the RNG is keyed by absolute step)."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec(name)
+  n, t = 200, 60
+
+  def run(th, sp):
+    eng = Engine(spec)
+    eng.init_chains(golden_init(name, n))
+    eng.set_rng('philox', seed=31)
+    eng.alloc_trace(t // th, th)
+    eng.run(t, steps_per_launch=sp)
+    tr, mom = eng.trace(), eng.moments()
+    eng.close()
+    return tr, mom
+
+  full, mf = run(1, 0)
+  part, mp = run(thin, spl)
+  for k in ('v_x', 'v_p', 'u'):
+    np.testing.assert_array_equal(part[k], full[k][:, thin - 1::thin])
+  np.testing.assert_array_equal(mp['n_acc'], mf['n_acc'])
+  np.testing.assert_allclose(mp['sum'], mf['sum'], rtol=1e-13, atol=1e-12)
