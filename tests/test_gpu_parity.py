@@ -360,3 +360,41 @@ def test_production_thinning_equals_every_kth_step(name, thin, spl):
     np.testing.assert_array_equal(part[k], full[k][:, thin - 1::thin])
   np.testing.assert_array_equal(mp['n_acc'], mf['n_acc'])
   np.testing.assert_allclose(mp['sum'], mf['sum'], rtol=1e-13, atol=1e-12)
+
+
+@pytest.mark.parametrize('name,n,t', [('gibbs8', 32768, 48), ('gmm2', 32768, 120)])
+def test_full_size_cfg3_cfg5_replay_parity(name, n, t):
+  """BASELINE cfg3 / cfg5 per-GPU widths in replay mode: 256 sampled chains
+  match the oracle step for step; trace/moment invariants hold for all."""
+  from probayes_amd.replay import legacy_streams_parallel
+  spec = oracle.golden_spec(name)
+  seeds = np.arange(n, dtype=np.int64) + 3_000_000
+  streams = legacy_streams_parallel(spec, t, seeds, processes=16)
+  init = golden_init(name, n)
+  out, mom = _run_replay(spec, init, streams, debug=False)
+  assert np.array_equal(mom['n_acc'], out['u'].sum(axis=1))
+  np.testing.assert_allclose(mom['sum'], out['v_x'].sum(axis=1), rtol=1e-12,
+                             atol=1e-9)
+  pick = np.random.RandomState(9).choice(n, 256, replace=False)
+  run = oracle.run_gibbs if spec['scores'] == 'gibbs' else oracle.run_mh
+  ref = run(spec, init[pick], streams[:, :, pick])
+  assert np.array_equal(out['u'][pick], ref['u'])
+  assert _rel_err(out['v_x'][pick], ref['v_x'], 1.) <= RTOL
+  assert _rel_err(out['v_p'][pick], ref['v_p']) <= RTOL
+
+
+@pytest.mark.parametrize('d,n', [(32, 70), (16, 1), (12, 33), (3, 1)])
+def test_extreme_dims_and_chain_counts_replay(d, n):
+  """Largest compiled dimension (32: lane-pair kernel with 16 dims per half),
+  a single chain, and ragged chain counts against the oracle."""
+  from oracle.workloads import spec_diag10
+  spec = spec_diag10({'mu': np.linspace(-1., 1., d),
+                      'sigma': np.linspace(0.5, 2., d), 'step': 0.5})
+  t = 40
+  streams = oracle.legacy_streams(spec, np.arange(n) + 11, t)
+  init = np.zeros((n, d))
+  out, _ = _run_replay(spec, init, streams, debug=False)
+  ref = oracle.run_mh(spec, init, streams)
+  assert np.array_equal(out['u'], ref['u'])
+  assert _rel_err(out['v_x'], ref['v_x'], 1.) <= RTOL
+  assert _rel_err(out['v_p'], ref['v_p']) <= RTOL
