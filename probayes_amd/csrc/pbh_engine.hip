@@ -58,6 +58,7 @@ struct pbh_engine {
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
   bool gibbs_fast = true;    // PBH_GIBBS_FAST=0 keeps the ndtri kernel for Philox
   int gibbs_lanes = 0;       // PBH_GIBBS_LANES: lanes per chain of that kernel
+  int gmm_lanes = 2;         // PBH_GMM_LANES: lanes per chain of the GMM kernel
   // MVN target on the host (for the production Gibbs tables)
   std::vector<double> mvn_mean, mvn_U;
   double mvn_const = 0.;
@@ -181,6 +182,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gm = std::getenv("PBH_GIBBS_MFMA")) e->gibbs_mfma = gm[0] != '0';
   if (const char *gf = std::getenv("PBH_GIBBS_FAST")) e->gibbs_fast = gf[0] != '0';
   if (const char *gl = std::getenv("PBH_GIBBS_LANES")) e->gibbs_lanes = std::atoi(gl);
+  if (const char *ml = std::getenv("PBH_GMM_LANES")) e->gmm_lanes = std::atoi(ml);
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -672,6 +674,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gibbs_mfma = e->gibbs_mfma ? 1 : 0;
   k.gibbs_fast = e->gibbs_fast ? 1 : 0;
   k.gibbs_lanes = e->gibbs_lanes;
+  k.gmm_lanes = e->gmm_lanes;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;

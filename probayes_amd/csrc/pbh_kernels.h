@@ -72,6 +72,7 @@ struct KArgs {
   double *gq;          // persisted g = P'(x - mu') [d][n] and Q [n]
   int32_t gq_init;     // 1: recompute g, Q from x at entry
   int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
+  int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
   // ---- moments ----
   double *msum, *msq;
   int64_t *nacc;

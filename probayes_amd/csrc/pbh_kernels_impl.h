@@ -619,6 +619,58 @@ __device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
   od = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
 }
 
+template <int L>
+__device__ __forceinline__ double part_sum(double v) {
+  // sum of v over the L lanes of a group, identical (same order) in each
+  if constexpr (L == 1) {
+    return v;
+  } else if constexpr (L == 2) {
+    double lo, hi;
+    halves_f64(v, lo, hi);
+    return lo + hi;
+  } else {
+    double ev, od, lo, hi;
+    rowpair_f64(v, ev, od);
+    halves_f64(ev + od, lo, hi);
+    return lo + hi;
+  }
+}
+
+template <int L, int Q>
+__device__ __forceinline__ double part_bcast(double v) {
+  // the value of part Q's lane of the group, in every lane of it
+  if constexpr (L == 1) {
+    return v;
+  } else if constexpr (L == 2) {
+    double lo, hi;
+    halves_f64(v, lo, hi);
+    return Q ? hi : lo;
+  } else {
+    double ev, od, lo, hi;
+    rowpair_f64(v, ev, od);
+    halves_f64((Q & 1) ? od : ev, lo, hi);
+    return (Q >> 1) ? hi : lo;
+  }
+}
+
+template <int L>
+__device__ __forceinline__ double part_max(double v) {
+  // maximum of v over the L lanes of a group (fmax: NaN-ignoring)
+  if constexpr (L == 1) {
+    return v;
+  } else if constexpr (L == 2) {
+    double lo, hi;
+    halves_f64(v, lo, hi);
+    return __builtin_fmax(lo, hi);
+  } else {
+    double ev, od, lo, hi;
+    rowpair_f64(v, ev, od);
+    halves_f64(__builtin_fmax(ev, od), lo, hi);
+    return __builtin_fmax(lo, hi);
+  }
+}
+
+
 
 // Production draws of a PAIR of half-steps (steps 2P, 2P + 1) of one lane:
 // NP = H / 2 Box-Muller pairs per step from NP Philox blocks (q < NP), and
@@ -899,36 +951,39 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Lane-pair MH kernel for the Gaussian-mixture target with the callable
+// Multi-lane MH kernel for the Gaussian-mixture target with the callable
 // Gaussian delta (cfg5, production RNG).  At d = 2 the one-chain-per-lane
 // kernel leaves every other SIMD idle at 32 768 chains; here one chain is a
-// lane PAIR (l, l + 32).  Both halves hold the whole state and draw the same
-// proposal (the same Philox block); the K components are split over the
-// halves (k = 2 kk + h), each half forms the log-sum-exp of its components,
-// and one exchange combines them: lse = M + log(s_M + s_m exp(m - M)).
-// Acceptance is the filtered ratio form, identical in both halves.
+// group of L lanes (rows of 64 / L lanes).  Every lane of a group holds the
+// whole state and draws the same proposal (the same Philox block); the K
+// components are dealt over the parts (k = p + L kk), each part forms its
+// partial log-sum-exp (m_p, s_p), and the group combines them:
+// lse = M + log(sum_p s_p exp(m_p - M)), M = max_p m_p.  Acceptance is the
+// filtered ratio form, identical in every lane of the group.
 // ---------------------------------------------------------------------------
-template <int D, int K>
-__global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
-  static_assert(K >= 2, "each half needs a component");
-  constexpr int KH = (K + 1) / 2;
+template <int D, int K, int L>
+__global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
+  constexpr int KL = (K + L - 1) / L;    // component slots per part
+  constexpr int CW = 64 / L;             // chains per wavefront
   constexpr double kNegInf = -__builtin_inf();
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   const int lane = threadIdx.x & 63;
-  const int h = lane >= 32 ? 1 : 0;
+  const int p = lane / CW;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const int64_t c = wave * 32 + (lane & 31);
+  const int64_t c = wave * CW + (lane % CW);
   const bool active = c < a.n;
   const int64_t cc = active ? c : 0;
   const uint64_t act_mask = __ballot(active);
   const int64_t chain = a.off + cc;
 
-  // this half's components k = 2 kk + h (a missing one contributes exp = 0)
-  double cw[KH], c0[KH], cmu[KH][D];
+  // this part's components k = p + L kk (a missing one contributes 0)
+  double cw[KL], c0[KL], cmu[KL][D];
+  bool any = false;
 #pragma unroll
-  for (int kk = 0; kk < KH; ++kk) {
-    const int k = 2 * kk + h;
+  for (int kk = 0; kk < KL; ++kk) {
+    const int k = p + L * kk;
     const bool ok = k < K;
+    any = any || ok;
     cw[kk] = ok ? a.tw[k] : 0.;
     c0[kk] = ok ? a.tw[K + k] : kNegInf;
 #pragma unroll
@@ -945,6 +1000,7 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
   int64_t nacc = 0;
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
 
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
@@ -978,10 +1034,10 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
 #pragma unroll
     for (int i = 0; i < D; ++i)
       xp[i] = x[i] + __builtin_fma(r[i], cld(a.pscl, i), cld(a.ploc, i));
-    // ---- log-sum-exp over this half's components, then the pair's ----
-    double v[KH];
+    // ---- partial log-sum-exp over this part's components, then the group's
+    double v[KL];
 #pragma unroll
-    for (int kk = 0; kk < KH; ++kk) {
+    for (int kk = 0; kk < KL; ++kk) {
       double acc = c0[kk];
 #pragma unroll
       for (int i = 0; i < D; ++i) {
@@ -992,18 +1048,13 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
     }
     double m = v[0];
 #pragma unroll
-    for (int kk = 1; kk < KH; ++kk) m = __builtin_fmax(m, v[kk]);
-    double sl = 0.;
+    for (int kk = 1; kk < KL; ++kk) m = __builtin_fmax(m, v[kk]);
+    const double M = part_max<L>(m);
+    double e = 0.;
 #pragma unroll
-    for (int kk = 0; kk < KH; ++kk) sl += fast_exp(v[kk] - m);
-    double m0, m1, s0, s1;
-    halves_f64(m, m0, m1);
-    halves_f64(sl, s0, s1);
-    const bool big0 = m0 >= m1;
-    const double e = fast_exp(-__builtin_fabs(m0 - m1));
-    const double S = big0 ? __builtin_fma(s1, e, s0) : __builtin_fma(s0, e, s1);
-    const double lpp = __builtin_fmax(m0, m1) + log(S);
-    // ---- acceptance (identical in both halves) ----
+    for (int kk = 0; kk < KL; ++kk) e += fast_exp(v[kk] - M);
+    const double lpp = M + log(part_sum<L>(any ? e : 0.));
+    // ---- acceptance (identical in every lane of the group) ----
     bool acc;
     if (!a.has_pred && s == 0) {
       acc = true;                                  // s = None on step 1
@@ -1021,7 +1072,7 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
     nacc += acc ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      if (i % 2 == h) {
+      if (i % L == p) {
         ms[i] += x[i];
         mq[i] = __builtin_fma(x[i], x[i], mq[i]);
       }
@@ -1035,24 +1086,28 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_pair_kernel(KArgs a) {
         double *row = a.tx + rec * D * a.n;
 #pragma unroll
         for (int i = 0; i < D; ++i)
-          if (i % 2 == h) __builtin_nontemporal_store(x[i], &row[i * a.n + c]);
-        if (h == 0) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
+          if (i % L == p) __builtin_nontemporal_store(x[i], &row[i * a.n + c]);
+        if (p == 0) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
       }
-      const uint64_t am = __ballot(acc) & act_mask;   // halves agree
-      if (lane == 0 && wave < 2 * a.W)
-        reinterpret_cast<uint32_t *>(a.tacc)[rec * 2 * a.W + wave] = (uint32_t)am;
+      // the parts agree: part 0's lanes (bits [0, CW)) carry the chains
+      const uint64_t am = __ballot(acc) & act_mask;
+      if (lane == 0 && wave < (64 / CW) * a.W) {   // stay inside the record
+        const int64_t wi = rec * (64 / CW) * a.W + wave;
+        if constexpr (CW == 32) reinterpret_cast<uint32_t *>(a.tacc)[wi] = (uint32_t)am;
+        else reinterpret_cast<uint16_t *>(a.tacc)[wi] = (uint16_t)am;
+      }
     }
   }
   if (active) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      if (i % 2 == h) {
+      if (i % L == p) {
         a.x[i * a.n + c] = x[i];
         a.msum[i * a.n + c] += ms[i];
         a.msq[i * a.n + c] += mq[i];
       }
     }
-    if (h == 0) {
+    if (p == 0) {
       a.lp[c] = lp;
       a.nacc[c] += nacc;
     }
@@ -1276,40 +1331,6 @@ __device__ __forceinline__ void gather_parts(const double (&own)[M],
     for (int i = 0; i < M; ++i) rowpair_f64(own[i], blk[i], blk[M + i]);
 #pragma unroll
     for (int j = 0; j < 2 * M; ++j) halves_f64(blk[j], all[j], all[2 * M + j]);
-  }
-}
-
-template <int L>
-__device__ __forceinline__ double part_sum(double v) {
-  // sum of v over the L lanes of a group, identical (same order) in each
-  if constexpr (L == 1) {
-    return v;
-  } else if constexpr (L == 2) {
-    double lo, hi;
-    halves_f64(v, lo, hi);
-    return lo + hi;
-  } else {
-    double ev, od, lo, hi;
-    rowpair_f64(v, ev, od);
-    halves_f64(ev + od, lo, hi);
-    return lo + hi;
-  }
-}
-
-template <int L, int Q>
-__device__ __forceinline__ double part_bcast(double v) {
-  // the value of part Q's lane of the group, in every lane of it
-  if constexpr (L == 1) {
-    return v;
-  } else if constexpr (L == 2) {
-    double lo, hi;
-    halves_f64(v, lo, hi);
-    return Q ? hi : lo;
-  } else {
-    double ev, od, lo, hi;
-    rowpair_f64(v, ev, od);
-    halves_f64((Q & 1) ? od : ev, lo, hi);
-    return (Q >> 1) ? hi : lo;
   }
 }
 
@@ -1685,14 +1706,26 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
   if constexpr (D <= 4) {
     if (a.target == PBH_TARGET_GMM && a.prop == PBH_PROP_GAUSS) {
       if (gmm_pair_form(a) && a.tn >= 2 && a.tn <= 4) {
-        const int64_t waves = (a.n + 31) / 32;
+        // lanes per chain: PBH_GMM_LANES (2 or 4), default 2 (measured:
+        // 4 lanes, each repeating the Philox block, are slower at cfg5)
+        const int L = a.gmm_lanes == 4 ? 4 : 2;
+        const int64_t waves = (a.n + 64 / L - 1) / (64 / L);
         const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
-        if (a.tn == 2)
-          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 2>), grid, block, 0, st, a);
-        else if (a.tn == 3)
-          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 3>), grid, block, 0, st, a);
-        else
-          hipLaunchKernelGGL((mh_gmm_pair_kernel<D, 4>), grid, block, 0, st, a);
+        if (L == 2) {
+          if (a.tn == 2)
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 2, 2>), grid, block, 0, st, a);
+          else if (a.tn == 3)
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 3, 2>), grid, block, 0, st, a);
+          else
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 4, 2>), grid, block, 0, st, a);
+        } else {
+          if (a.tn == 2)
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 2, 4>), grid, block, 0, st, a);
+          else if (a.tn == 3)
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 3, 4>), grid, block, 0, st, a);
+          else
+            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 4, 4>), grid, block, 0, st, a);
+        }
         return hipGetLastError();
       }
       launch_mh_spec<D, PBH_TARGET_GMM, PBH_PROP_GAUSS>(a, st, lds);

@@ -307,15 +307,17 @@ def test_production_modes_agree_with_reference_arithmetic(name):
   assert abs(a1 - a0) < 0.02, (a1, a0)
 
 
-def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch):
-  """cfg5 form: the lane-pair GMM kernel (components split over the halves)
-  draws the same Philox stream as the one-chain-per-lane kernel; its
+@pytest.mark.parametrize('lanes', ['2', '4'])
+def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch, lanes):
+  """cfg5 form: the multi-lane GMM kernel (components dealt over 2 or 4
+  lanes) draws the same Philox stream as the one-chain-per-lane kernel; its
   log-sum-exp differs only in rounding, so chains, accept bits and moments
   agree and log-densities agree to ~1e-14 (ragged chain count)."""
   from probayes_amd import Engine
   spec = oracle.golden_spec('gmm2')
   n, t = 3000, 300
   outs = {}
+  monkeypatch.setenv('PBH_GMM_LANES', lanes)
   for no_pair in ('0', '1'):
     monkeypatch.setenv('PBH_NO_PAIR', no_pair)
     eng = Engine(spec)
