@@ -203,6 +203,12 @@ int pbh_check_accept(int device, int64_t n, const double *lp,
                      const double *lpp, const uint32_t *t0, const uint32_t *t1,
                      int32_t lin, uint8_t *out);
 
+/* Evaluates the production Gibbs kernel's fp64 Box-Muller (box_muller_fast:
+ * the cheap log / sin / cos) and the libm form on n Philox-like blocks
+ * words[n][4]; fast[n][2], ref[n][2] receive (z0, z1) of each.             */
+int pbh_check_normals(int device, int64_t n, const uint32_t *words,
+                      double *fast, double *ref);
+
 #ifdef __cplusplus
 }
 #endif

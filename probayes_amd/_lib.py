@@ -98,6 +98,8 @@ SIGNATURES = {
     'pbh_rccl_destroy': (ctypes.c_int, [ctypes.c_void_p]),
     'pbh_check_accept': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _dp, _dp,
                                         _u32p, _u32p, ctypes.c_int32, _u8p]),
+    'pbh_check_normals': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _u32p,
+                                         _dp, _dp]),
 }
 
 

@@ -92,6 +92,83 @@ __device__ __forceinline__ void box_muller(u32x4 w, double &z0, double &z1) {
   z1 = r * s;
 }
 
+// fp64 log for u in [2^-53, 1] (the Box-Muller magnitude): u = 2^e m with m
+// in [sqrt(1/2), sqrt(2)), log m = 2 atanh(t), t = (m - 1) / (m + 1),
+// |t| <= 0.1716, 12 series terms (truncation < 1e-17); ~35 VALU against ~100
+// for the general libm log (special cases, denormals).  Within 2 ulp.
+__device__ __forceinline__ double log_unit(double u) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, u);
+  int e = (int)((b >> 52) & 0x7FF) - 1023;
+  double m = __builtin_bit_cast(double, (b & 0x000FFFFFFFFFFFFFull) |
+                                            0x3FF0000000000000ull);
+  const bool big = m > 1.4142135623730951;
+  m = big ? m * 0.5 : m;
+  e += big ? 1 : 0;
+  const double t = (m - 1.0) / (m + 1.0);
+  const double s = t * t;
+  double p = 1.0 / 23.0;
+  p = __builtin_fma(p, s, 1.0 / 21.0);
+  p = __builtin_fma(p, s, 1.0 / 19.0);
+  p = __builtin_fma(p, s, 1.0 / 17.0);
+  p = __builtin_fma(p, s, 1.0 / 15.0);
+  p = __builtin_fma(p, s, 1.0 / 13.0);
+  p = __builtin_fma(p, s, 1.0 / 11.0);
+  p = __builtin_fma(p, s, 1.0 / 9.0);
+  p = __builtin_fma(p, s, 1.0 / 7.0);
+  p = __builtin_fma(p, s, 1.0 / 5.0);
+  p = __builtin_fma(p, s, 1.0 / 3.0);
+  p = __builtin_fma(p, s, 1.0);
+  const double lm = 2.0 * t * p;
+  const double de = (double)e;
+  return __builtin_fma(de, 6.93147180369123816490e-01,
+                       __builtin_fma(de, 1.90821492927058770002e-10, lm));
+}
+
+// (sin, cos)(2 pi u) for u in [0, 1): quadrant q = round(4u) mod 4, reduced
+// angle phi = (4u - round(4u)) pi / 2 in [-pi/4, pi/4] (4u is exact), Taylor
+// polynomials to phi^15 / phi^16 (truncation < 1e-17).  ~30 VALU against
+// ~70 for sincospi.  Within 2 ulp.
+__device__ __forceinline__ void sincos_2pi(double u, double &sn, double &cs) {
+  const double v = 4.0 * u;
+  const double k = __builtin_rint(v);
+  const double phi = (v - k) * 1.5707963267948966;
+  const double f = phi * phi;
+  double ps = -7.6471637318198164759e-13;               // -1/15!
+  ps = __builtin_fma(ps, f, 1.6059043836821614599e-10);  //  1/13!
+  ps = __builtin_fma(ps, f, -2.5052108385441718775e-08); // -1/11!
+  ps = __builtin_fma(ps, f, 2.7557319223985890653e-06);  //  1/9!
+  ps = __builtin_fma(ps, f, -1.9841269841269841270e-04); // -1/7!
+  ps = __builtin_fma(ps, f, 8.3333333333333333333e-03);  //  1/5!
+  ps = __builtin_fma(ps, f, -1.6666666666666666667e-01); // -1/3!
+  const double sp = __builtin_fma(ps * f, phi, phi);
+  double pc = 4.7794773323873852974e-14;                 //  1/16!
+  pc = __builtin_fma(pc, f, -1.1470745597729724714e-11); // -1/14!
+  pc = __builtin_fma(pc, f, 2.0876756987868098979e-09);  //  1/12!
+  pc = __builtin_fma(pc, f, -2.7557319223985890653e-07); // -1/10!
+  pc = __builtin_fma(pc, f, 2.4801587301587301587e-05);  //  1/8!
+  pc = __builtin_fma(pc, f, -1.3888888888888888889e-03); // -1/6!
+  pc = __builtin_fma(pc, f, 4.1666666666666666667e-02);  //  1/4!
+  pc = __builtin_fma(pc, f, -0.5);                       // -1/2!
+  const double cp = __builtin_fma(pc, f, 1.0);
+  const int q = ((int)k) & 3;
+  const double s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
+  sn = (q & 2) ? -s0 : s0;
+  cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
+// Two standard normals from one Philox block in fp64 with the cheap log and
+// sin/cos above (the Gibbs production kernel's draws): the same (u1, u2) as
+// box_muller, values within a few ulp of it.
+__device__ __forceinline__ void box_muller_fast(u32x4 w, double &z0, double &z1) {
+  const double u1 = 1.0 - u01(w.x, w.y);  // (0, 1]
+  const double u2 = u01(w.z, w.w);
+  const double r = sqrt(-2.0 * log_unit(u1));
+  double s, c;
+  sincos_2pi(u2, s, c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
 // Production normals (PBH_RNG_PHILOX): two standard-normal pairs per Philox
 // block from the hardware fp32 transcendentals (v_log_f32, v_sin_f32,
 // v_cos_f32), widened to fp64.  The magnitude r = sqrt(-2 ln u1) uses 24-bit

@@ -914,4 +914,29 @@ int pbh_check_accept(int device, int64_t n, const double *lp,
   return PBH_OK;
 }
 
+int pbh_check_normals(int device, int64_t n, const uint32_t *words,
+                      double *fast, double *ref) {
+  if (check_ptr(words, "words") || check_ptr(fast, "fast") || check_ptr(ref, "ref"))
+    return PBH_ERR_ARG;
+  if (n <= 0) return fail(PBH_ERR_ARG, "n must be positive");
+  HIP_TRY(hipSetDevice(device));
+  uint32_t *dw = nullptr;
+  double *df = nullptr, *dr = nullptr;
+  int rc = dalloc(dw, 4 * n);
+  if (!rc) rc = dalloc(df, 2 * n);
+  if (!rc) rc = dalloc(dr, 2 * n);
+  hipError_t err = hipSuccess;
+  if (!rc) {
+    err = hipMemcpy(dw, words, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = pbh::launch_check_normals(n, dw, df, dr);
+    if (err == hipSuccess) err = hipMemcpy(fast, df, 2 * n * sizeof(double), hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(ref, dr, 2 * n * sizeof(double), hipMemcpyDeviceToHost);
+  }
+  dfree(dw); dfree(df); dfree(dr);
+  if (rc) return rc;
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_check_normals: %s", hipGetErrorString(err));
+  return PBH_OK;
+}
+
 }  // extern "C"

@@ -90,6 +90,8 @@ hipError_t launch_gibbs(const KArgs &a, hipStream_t s);
 hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
                           hipStream_t s);
 bool mh_dim_supported(int d);
+hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
+                                double *ref);
 hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
                                const uint32_t *t0, const uint32_t *t1,
                                int32_t lin, double log_npi, uint8_t *out);

@@ -1401,8 +1401,8 @@ struct GibbsFast {
 #pragma unroll
     for (int b = 0; b < (M + 1) / 2; ++b) {
       double z0, z1;
-      box_muller(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain), a.seed_lo,
-                               a.seed_hi), z0, z1);
+      box_muller_fast(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain),
+                                    a.seed_lo, a.seed_hi), z0, z1);
       zo[2 * b] = z0;
       if (2 * b + 1 < M) zo[2 * b + 1] = z1;
     }
