@@ -5,10 +5,58 @@ probability `prob` in a given `pscale`; SP.__call__(samples) summates the
 per-step PDs into 1-D arrays (pd_utils.py:332-411).  Here the values are the
 engine's trace arrays -- [T] for a single chain, [T, N] for a batched sampler
 -- and no per-step object is ever built on the hot path.
+
+Summary operations: expectation, sorted, quantile and
+marginal with the reference's semantics (pd.py:168-211, 373-493) on the
+sample axis -- axis 0, so a batched [T, N] summary is treated chain by
+chain.  Pinned by tests/golden/pd_ops.npz (tools/gen_pd_golden.py).
 """
 import numpy as np
 
-from probayes_amd.pscales import rescale
+from probayes_amd.pscales import NEARLY_POSITIVE_ZERO, rescale
+
+
+def _div_prob(dividend, divisor):
+  """pscales.py:219-236 on linear arrays."""
+  return dividend / np.maximum(NEARLY_POSITIVE_ZERO, divisor)
+
+
+def _ismonotonic(vals):
+  """pd_utils.py:414-421."""
+  vals = np.ravel(vals)
+  if vals.size <= 1:
+    return True
+  return len(np.unique(vals[1:] >= vals[:-1])) == 1
+
+
+def _quantile_1d(vals, prob, pscale, quants):
+  """pd.py:408-460 for one chain's samples (1-D values of every key)."""
+  unsorted = {k for k, v in vals.items() if not _ismonotonic(v)}
+  ravprob = rescale(np.ravel(np.asarray(prob, float)), pscale, 'lin')
+  cumprob = np.cumsum(ravprob)
+  cumprob = _div_prob(cumprob, cumprob[-1])
+  cum_idx = np.maximum(0, np.digitize(np.array(quants), cumprob) - 1).tolist()
+  out = []
+  for j, rav_idx in enumerate(cum_idx):
+    rav_idx = int(rav_idx)
+    qd = {}
+    for key, v in vals.items():
+      v = np.ravel(v)
+      if key in unsorted:
+        qd[key] = {v.size}
+        continue
+      idx = min(rav_idx, len(v) - 1)
+      if idx == len(v) - 1:
+        qd[key] = v[idx]
+        continue
+      vv = v[idx:idx + 2]
+      ravp = ravprob[rav_idx:rav_idx + 2]
+      if np.abs(np.diff(ravp)) < min(quants[j], 1. - quants[j]):
+        qd[key] = np.interp(quants[j], cumprob[rav_idx:rav_idx + 2], vv)
+      else:
+        qd[key] = np.sum(ravp * vv) / np.sum(ravp)
+    out.append(qd)
+  return out
 
 
 class PD(dict):
@@ -29,6 +77,63 @@ class PD(dict):
     prob = None if self.prob is None else \
         rescale(np.copy(self.prob), self.pscale, pscale)
     return PD(self.name, dict(self), prob=prob, pscale=pscale)
+
+  def _lin_prob(self):
+    return rescale(np.asarray(self.prob, float), self.pscale, 'lin')
+
+  def expectation(self, keys=None, exponent=None):
+    """pd.py:373-405: probability-weighted mean over the sample axis,
+    sum(p v^exponent) / sum(p) with p rescaled to linear."""
+    keys = list(self.keys()) if keys is None else \
+        ([keys] if isinstance(keys, str) else list(keys))
+    for key in keys:
+      assert key in self, 'Key {} not marginal in distribution {}'.format(
+          key, self.name)
+    prob = self._lin_prob()
+    sum_prob = np.sum(prob, axis=0)
+    out = {}
+    for key in keys:
+      val = np.asarray(self[key], float)
+      val = val ** exponent if exponent else val
+      out[key] = _div_prob(np.sum(prob * val, axis=0), sum_prob)
+    return out
+
+  def sorted(self, key):
+    """pd.py:463-493: samples reordered by the values of key (argsort along
+    the sample axis, per chain when batched)."""
+    idx = np.argsort(np.asarray(self[key]), axis=0)
+    take = lambda a: np.take_along_axis(np.asarray(a), idx, axis=0)
+    vals = {k: take(v) for k, v in self.items()}
+    return PD(self.name, vals, prob=take(self.prob), pscale=self.pscale)
+
+  def quantile(self, q=0.5):
+    """pd.py:408-460: quantiles of the probability-weighted samples, for
+    keys whose values are sorted (others give {size}); batched summaries
+    return one dict per chain."""
+    scalar = np.isscalar(q)
+    quants = [q] if scalar else list(q)
+    prob = np.asarray(self.prob, float)
+    if prob.ndim <= 1:
+      res = _quantile_1d(dict(self), prob, self.pscale, quants)
+      return res[0] if scalar else res
+    per_chain = []
+    for c in range(prob.shape[1]):
+      vals = {k: np.asarray(v)[:, c] for k, v in self.items()}
+      res = _quantile_1d(vals, prob[:, c], self.pscale, quants)
+      per_chain.append(res[0] if scalar else res)
+    return per_chain
+
+  def marginal(self, keys):
+    """pd.py:168-211 for a summary, whose variables share the sample axis:
+    only the marginal of all of them exists."""
+    keys = {keys} if isinstance(keys, str) else set(keys)
+    for key in keys:
+      assert key in self, 'Key {} not marginal in distribution {}'.format(
+          key, self.name)
+    assert keys == set(self.keys()), \
+        'Dimensionality precludes marginalising {} without: {}'.format(
+            keys, set(self.keys()) - keys)
+    return PD(self.name, dict(self), prob=self.prob, pscale=self.pscale)
 
   def __repr__(self):
     keys = ','.join(self.keys())
