@@ -22,6 +22,8 @@ step workloads 240 python scripts/bench_workloads.py
 [ -x tools/ubench/store_pattern ] && step store_pattern 120 tools/ubench/store_pattern
 step gibbs_lanes4 120 env PBH_GIBBS_LANES=4 python scripts/bench_workloads.py --only cfg3
 step gibbs_ndtri 120 env PBH_GIBBS_FAST=0 python scripts/bench_workloads.py --only cfg3
+step gibbs_ndtri_valu 120 env PBH_GIBBS_FAST=0 PBH_GIBBS_MFMA=0 python scripts/bench_workloads.py --only cfg3
+step gmm_lanes4 120 env PBH_GMM_LANES=4 python scripts/bench_workloads.py --only cfg5
 P=$O/prof; mkdir -p $P; cd /tmp
 A="--steps 1000 --warmup 250 --no-cpu-baseline"
 step prof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- python3 $R/bench.py $A
