@@ -188,7 +188,8 @@ int pbh_rccl_unique_id(uint8_t id[128]);
 int pbh_rccl_init(pbh_engine *eng, int32_t rank, int32_t world,
                   const uint8_t id[128]);
 /* Gathers every rank's moments ([2d+1][N_local] doubles, n_acc as double)
- * into out [world][2d+1][N_local] on the host.                              */
+ * into out [world][2d+1][N_local] on the host.  Every rank must hold the
+ * same N_local (PBH_ERR_ARG otherwise; pad the chain set to shard evenly). */
 int pbh_rccl_allgather_moments(pbh_engine *eng, double *out);
 /* Max-reduces one double over ranks (bench timing).                         */
 int pbh_rccl_allreduce_max(pbh_engine *eng, double *value);

@@ -841,6 +841,31 @@ int pbh_rccl_allgather_moments(pbh_engine *e, double *out) {
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   HIP_TRY(hipSetDevice(e->device));
   const int64_t n = e->n, dn = (int64_t)e->d * n, cnt = 2 * dn + n;
+  {
+    // ncclAllGather needs one count on every rank: refuse ragged shards
+    // (a mismatch would hang the collective) -- max(n) == -max(-n)
+    int rc0 = e->scalar ? PBH_OK : dalloc(e->scalar, 1);
+    if (rc0) return rc0;
+    double lim[2] = {(double)n, -(double)n};
+    double *dl = nullptr;
+    rc0 = dalloc(dl, 2);
+    if (rc0) return rc0;
+    hipError_t err = hipMemcpy(dl, lim, sizeof lim, hipMemcpyHostToDevice);
+    ncclResult_t nr = ncclSuccess;
+    if (err == hipSuccess)
+      nr = ncclAllReduce(dl, dl, 2, ncclFloat64, ncclMax, e->comm, e->stream);
+    if (err == hipSuccess && nr == ncclSuccess) err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess && nr == ncclSuccess)
+      err = hipMemcpy(lim, dl, sizeof lim, hipMemcpyDeviceToHost);
+    dfree(dl);
+    if (nr != ncclSuccess)
+      return fail(PBH_ERR_RCCL, "chain-count check failed: %s", ncclGetErrorString(nr));
+    HIP_TRY(err);
+    if (lim[0] != -lim[1])
+      return fail(PBH_ERR_ARG,
+                  "all-gather needs equal chain counts on every rank (%g..%g)",
+                  -lim[1], lim[0]);
+  }
   int rc = dalloc(e->gather_send, cnt);
   if (!rc) rc = dalloc(e->gather_recv, (size_t)cnt * e->world);
   if (rc) return rc;
