@@ -92,10 +92,11 @@ __device__ __forceinline__ void box_muller(u32x4 w, double &z0, double &z1) {
   z1 = r * s;
 }
 
-// fp64 log for u in [2^-53, 1] (the Box-Muller magnitude): u = 2^e m with m
-// in [sqrt(1/2), sqrt(2)), log m = 2 atanh(t), t = (m - 1) / (m + 1),
-// |t| <= 0.1716, 12 series terms (truncation < 1e-17); ~35 VALU against ~100
-// for the general libm log (special cases, denormals).  Within 2 ulp.
+// fp64 log of a positive normal double (the Box-Muller magnitude takes u in
+// [2^-53, 1]): u = 2^e m with m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(t),
+// t = (m - 1) / (m + 1), |t| <= 0.1716, 12 series terms (truncation
+// < 1e-17); ~35 VALU against ~100 for the general libm log (special cases,
+// denormals).  Within 2 ulp.
 __device__ __forceinline__ double log_unit(double u) {
   const uint64_t b = __builtin_bit_cast(uint64_t, u);
   int e = (int)((b >> 52) & 0x7FF) - 1023;
@@ -122,6 +123,16 @@ __device__ __forceinline__ double log_unit(double u) {
   const double de = (double)e;
   return __builtin_fma(de, 6.93147180369123816490e-01,
                        __builtin_fma(de, 1.90821492927058770002e-10, lm));
+}
+
+// fp64 log of any double for the production paths: log_unit's series on
+// positive normal numbers; zero, negatives, denormals, inf and NaN take the
+// libm log (a divergent branch that is never entered for model values).
+__device__ __forceinline__ double fast_log(double x) {
+  const bool normal = x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308;
+  double r = log_unit(normal ? x : 1.0);
+  if (!normal) r = log(x);
+  return r;
 }
 
 // (sin, cos)(2 pi u) for u in [0, 1): quadrant q = round(4u) mod 4, reduced

@@ -172,7 +172,7 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
         if (k == a.i0) mu = x[k];
         if (k == a.i1) sg = x[k];
       }
-      const double lsg = log(sg);
+      const double lsg = FAST ? fast_log(sg) : log(sg);
       const double logC = a.norm_logC;
       if (FAST) {
         // production path: sufficient statistics (obar, S2) of the data
@@ -490,7 +490,9 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < D; ++k)
-        xp[k] = ((a.ufun >> k) & 1u) ? exp(log(x[k]) + dl[k]) : x[k] + dl[k];
+        xp[k] = ((a.ufun >> k) & 1u)
+                    ? (FAST ? fast_exp(fast_log(x[k]) + dl[k]) : exp(log(x[k]) + dl[k]))
+                    : x[k] + dl[k];
     }
     // ---- density, score, accept ----
     const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
