@@ -135,47 +135,85 @@ __device__ __forceinline__ double fast_log(double x) {
   return r;
 }
 
-// (sin, cos)(2 pi u) for u in [0, 1): quadrant q = round(4u) mod 4, reduced
-// angle phi = (4u - round(4u)) pi / 2 in [-pi/4, pi/4] (4u is exact), Taylor
-// polynomials to phi^15 / phi^16 (truncation < 1e-17).  ~30 VALU against
-// ~70 for sincospi.  Within 2 ulp.
-__device__ __forceinline__ void sincos_2pi(double u, double &sn, double &cs) {
-  const double v = 4.0 * u;
-  const double k = __builtin_rint(v);
-  const double phi = (v - k) * 1.5707963267948966;
-  const double f = phi * phi;
-  double ps = -7.6471637318198164759e-13;               // -1/15!
-  ps = __builtin_fma(ps, f, 1.6059043836821614599e-10);  //  1/13!
-  ps = __builtin_fma(ps, f, -2.5052108385441718775e-08); // -1/11!
-  ps = __builtin_fma(ps, f, 2.7557319223985890653e-06);  //  1/9!
-  ps = __builtin_fma(ps, f, -1.9841269841269841270e-04); // -1/7!
+// Table-driven fp64 Box-Muller for the Gibbs production kernel: log and
+// (sin, cos)(2 pi u) from small LDS tables plus short polynomials.
+//   log u = e ln2 + log c_j + log1p(r), c_j = 1 + j/128 (top 7 mantissa
+//           bits), r = m / c_j - 1 in [0, 1/128): degree 7 (truncation 2e-18);
+//           in [1/2, 1) the table holds log(c_j / 2) itself (no cancellation
+//           against ln 2), and above 1 - 1/128 the series takes r = u - 1
+//           (exact) so that log u keeps its relative accuracy as u -> 1;
+//   (sin, cos)(2 pi u) = rotation of the table angle j / 256 turn by
+//           theta = 2 pi (u - j/256) < 0.0246: degrees 7 / 8.
+// Values within a few ulp of the libm form (tests/test_gpu_normals.py).
+struct BMTables {
+  double logc[128], logh[128], invc[128], sn[256], cs[256];
+};
+
+__device__ __forceinline__ void bm_tables_init(BMTables *t) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    if (i < 128) {
+      const double c = 1.0 + i / 128.0;
+      t->logc[i] = log(c);
+      t->logh[i] = log(0.5 * c);
+      t->invc[i] = 1.0 / c;
+    }
+    double sv, cv;
+    sincospi(i / 128.0, &sv, &cv);
+    t->sn[i] = sv;
+    t->cs[i] = cv;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double log_tab(double u, const BMTables *t) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, u);
+  const int e = (int)((b >> 52) & 0x7FF) - 1023;
+  const uint64_t mb = b & 0x000FFFFFFFFFFFFFull;
+  const int j = (int)(mb >> 45);
+  const double m = __builtin_bit_cast(double, mb | 0x3FF0000000000000ull);
+  const bool near1 = u > 0.9921875;   // 1 - 1/128
+  const double r = near1 ? u - 1.0 : __builtin_fma(m, t->invc[j], -1.0);
+  double p = 1.0 / 7.0;
+  p = __builtin_fma(p, r, -1.0 / 6.0);
+  p = __builtin_fma(p, r, 1.0 / 5.0);
+  p = __builtin_fma(p, r, -1.0 / 4.0);
+  p = __builtin_fma(p, r, 1.0 / 3.0);
+  p = __builtin_fma(p, r, -0.5);
+  const double l1p = __builtin_fma(p * r, r, r);
+  const double de = (double)e;
+  const double base = e == -1 ? t->logh[j]
+                              : __builtin_fma(de, 6.93147180369123816490e-01,
+                                              __builtin_fma(de, 1.90821492927058770002e-10,
+                                                            t->logc[j]));
+  return near1 ? l1p : base + l1p;
+}
+
+__device__ __forceinline__ void sincos_tab(double u, const BMTables *t,
+                                           double &sn, double &cs) {
+  const int j = (int)(u * 256.0);
+  const double th = (u - j * (1.0 / 256.0)) * 6.283185307179586;
+  const double f = th * th;
+  double ps = -1.9841269841269841270e-04;               // -1/7!
   ps = __builtin_fma(ps, f, 8.3333333333333333333e-03);  //  1/5!
   ps = __builtin_fma(ps, f, -1.6666666666666666667e-01); // -1/3!
-  const double sp = __builtin_fma(ps * f, phi, phi);
-  double pc = 4.7794773323873852974e-14;                 //  1/16!
-  pc = __builtin_fma(pc, f, -1.1470745597729724714e-11); // -1/14!
-  pc = __builtin_fma(pc, f, 2.0876756987868098979e-09);  //  1/12!
-  pc = __builtin_fma(pc, f, -2.7557319223985890653e-07); // -1/10!
-  pc = __builtin_fma(pc, f, 2.4801587301587301587e-05);  //  1/8!
+  const double st = __builtin_fma(ps * f, th, th);
+  double pc = 2.4801587301587301587e-05;                 //  1/8!
   pc = __builtin_fma(pc, f, -1.3888888888888888889e-03); // -1/6!
   pc = __builtin_fma(pc, f, 4.1666666666666666667e-02);  //  1/4!
   pc = __builtin_fma(pc, f, -0.5);                       // -1/2!
-  const double cp = __builtin_fma(pc, f, 1.0);
-  const int q = ((int)k) & 3;
-  const double s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
-  sn = (q & 2) ? -s0 : s0;
-  cs = ((q + 1) & 2) ? -c0 : c0;
+  const double ct = __builtin_fma(pc, f, 1.0);
+  const double sj = t->sn[j], cj = t->cs[j];
+  sn = __builtin_fma(sj, ct, cj * st);
+  cs = __builtin_fma(cj, ct, -(sj * st));
 }
 
-// Two standard normals from one Philox block in fp64 with the cheap log and
-// sin/cos above (the Gibbs production kernel's draws): the same (u1, u2) as
-// box_muller, values within a few ulp of it.
-__device__ __forceinline__ void box_muller_fast(u32x4 w, double &z0, double &z1) {
+__device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
+                                               double &z0, double &z1) {
   const double u1 = 1.0 - u01(w.x, w.y);  // (0, 1]
   const double u2 = u01(w.z, w.w);
-  const double r = sqrt(-2.0 * log_unit(u1));
+  const double r = sqrt(-2.0 * log_tab(u1, t));
   double s, c;
-  sincos_2pi(u2, s, c);
+  sincos_tab(u2, t, s, c);
   z0 = r * c;
   z1 = r * s;
 }

@@ -101,10 +101,12 @@ hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
 // Diagnostic: box_muller_fast against box_muller on caller-supplied blocks.
 __global__ void check_normals_kernel(int64_t n, const uint32_t *words,
                                      double *fast, double *ref) {
+  __shared__ BMTables t;
+  bm_tables_init(&t);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const u32x4 w{words[4 * i], words[4 * i + 1], words[4 * i + 2], words[4 * i + 3]};
-  box_muller_fast(w, fast[2 * i], fast[2 * i + 1]);
+  box_muller_tab(w, &t, fast[2 * i], fast[2 * i + 1]);
   box_muller(w, ref[2 * i], ref[2 * i + 1]);
 }
 

@@ -1398,13 +1398,15 @@ struct GibbsFast {
 
   // The normals of this lane's coordinates [p M, p M + M) for the coordinate
   // cycle starting at step gc, from Philox blocks 0x100 + 16 p + b.
+  const BMTables *bmt;   // LDS tables of the normals' log and sin / cos
+
   __device__ __forceinline__ void draw_cycle(const KArgs &a, int64_t gc,
                                              int64_t chain) {
 #pragma unroll
     for (int b = 0; b < (M + 1) / 2; ++b) {
       double z0, z1;
-      box_muller_fast(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain),
-                                    a.seed_lo, a.seed_hi), z0, z1);
+      box_muller_tab(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain),
+                                   a.seed_lo, a.seed_hi), bmt, z0, z1);
       zo[2 * b] = z0;
       if (2 * b + 1 < M) zo[2 * b + 1] = z1;
     }
@@ -1566,7 +1568,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L == 4 &
 void gibbs_fast_kernel(KArgs a) {
   using S = GibbsFastRun<D, L>;
   constexpr int M = S::M, CW = S::CW;
+  __shared__ BMTables s_bmt;
+  bm_tables_init(&s_bmt);
   S st;
+  st.bmt = &s_bmt;
   st.lane = threadIdx.x & 63;
   st.wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   st.c = st.wave * CW + (st.lane % CW);

@@ -62,7 +62,10 @@ def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--only', default='cfg1,cfg3,cfg5',
                   help='comma-separated subset of cfg1,cfg3,cfg5')
-  only = ap.parse_args().only.split(',')
+  ap.add_argument('--no-trace', action='store_true',
+                  help='cfg3 without the trace (arithmetic-only probe)')
+  args = ap.parse_args()
+  only = args.only.split(',')
   lines = []
   if 'cfg1' in only:
     eng, o = run('metrohast_norm1d', 128, 2000)
@@ -72,7 +75,7 @@ def main():
     eng.close()
     lines.append(dict(o, config='cfg1 model at 65536 chains'))
   if 'cfg3' in only:
-    eng, o = run('gibbs8', 32768, 8 * 256)
+    eng, o = run('gibbs8', 32768, 8 * 256, trace=not args.no_trace)
     o['coordinate_steps_per_s'] = o.pop('chain_steps_per_s')
     o['hbm_gbs'] = o['coordinate_steps_per_s'] * (8 * 8 + 8 + 1 / 8) / 1e9
     eng.close()

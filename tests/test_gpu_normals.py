@@ -1,5 +1,5 @@
-"""The production Gibbs kernel's fp64 Box-Muller (pbh_device.h box_muller_fast:
-atanh-series log on [2^-53, 1], Taylor sin/cos of the reduced quarter turn)
+"""The production Gibbs kernel's fp64 Box-Muller (pbh_device.h box_muller_tab:
+log and sin/cos from LDS tables plus short polynomials)
 against the libm form (box_muller: ocml log / sincospi) and against NumPy on
 the host, on random and extreme Philox-like words."""
 import numpy as np
