@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PBH_ABI_VERSION 1
+#define PBH_ABI_VERSION 2
 #define PBH_MAX_DIM 32
 
 #define PBH_OK 0
@@ -117,6 +117,11 @@ typedef struct pbh_proposal {
   double delta;             /* SPHERE: delta (already * rss if scale=True)    */
   const double *lengths;    /* SPHERE: per-dim multiplier (lengths or 1)      */
   const double *delta_vec;  /* UNIFORM: delta[d]                              */
+  /* Optional covariance-matrix random walk (any kind): the base delta is
+   * multiplied by tfun[d*d] (row-major), i.e. delta' = tfun . delta, as
+   * RF.eval_delta does with the Cholesky factor that RF.set_tran(ndarray)
+   * installs (rf.py:210-220, 340-354).  NULL = no tfun.                    */
+  const double *tfun;
 } pbh_proposal;
 
 /* CondCov Gibbs tables (replaces CondCov.__init__ + RF.eval_tfun cycling:

@@ -44,7 +44,24 @@ def div_prob(dividend, divisor, pscale):
 # Proposal (delta) forms
 # ----------------------------------------------------------------------------
 def eval_delta(spec, draws):
-  """draws: [R-1 or d, N] of this step's delta randoms -> delta [d, N]."""
+  """draws: [R-1 or d, N] of this step's delta randoms -> delta [d, N].
+
+  A covariance-matrix tran (proposal['tfun'], the Cholesky factor that
+  RF.set_tran(ndarray) installs, rf.py:210-220) multiplies the base delta of
+  every chain: tfun().dot(delta) (rf.py:340-354), one np.dot per chain as the
+  reference makes it."""
+  delta = _base_delta(spec, draws)
+  tf = spec['proposal'].get('tfun')
+  if tf is None:
+    return delta
+  tf = np.asarray(tf, np.float64)
+  out = np.empty_like(delta)
+  for c in range(delta.shape[1]):
+    out[:, c] = tf.dot(np.array(delta[:, c], dtype=float))
+  return out
+
+
+def _base_delta(spec, draws):
   prop, d = spec['proposal'], int(spec['dim'])
   kind = prop['kind']
   if kind == 'gauss':

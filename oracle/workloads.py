@@ -160,12 +160,41 @@ def spec_gmm2(params):
                _gauss(2, float(params['step'])))
 
 
+def spec_covrw2(params):
+  """examples/cov/multinorm_rw.py:6-15 model with a covariance RW proposal
+  (tests/mcmc_examples.py covrw2): mvn target, callable N(0, step^2) Delta,
+  tfun = chol(cov) (rf.py:210-220, 340-354).  The non-callable tran evaluates
+  to the default conditional 1. of the RF's linear pscale (rf.py:20,510-511);
+  the subfield route (sd.py:97-105) leaves the SP's _sym_tran False
+  (rf.py:179), so hastings takes the reverse branch with r = q (rf.py:536):
+  q~ = r~ = rescale(1., pscale) -- e under a log pscale (App. A-1)."""
+  cov = np.array([[1.5, -1.0], [-1.0, 2.]])
+  prop = _gauss(2, float(params['step']))
+  prop['tfun'] = np.linalg.cholesky(cov)
+  return _spec(2, ['x', 'y'], {'kind': 'mvn', 'mean': np.array([0.5, -0.5]),
+                               'cov': cov}, prop, pscale='lin',
+               tran={'kind': 'const', 'value': 1.0, 'sym': False})
+
+
+def spec_covrw5(params):
+  """tests/mcmc_examples.py covrw5: 5-dim diagonal Gaussian, spherical tuple
+  delta times chol(cov); tran as spec_covrw2 (e-tempered: log pscale)."""
+  d = len(params['mu'])
+  return _spec(d, ['x{}'.format(i) for i in range(d)],
+               {'kind': 'diag_gauss', 'mu': np.asarray(params['mu'], float),
+                'sigma': np.asarray(params['sigma'], float)},
+               {'kind': 'sphere', 'delta': float(params['step']),
+                'lengths': np.ones(d),
+                'tfun': np.linalg.cholesky(np.asarray(params['cov'], float))},
+               tran={'kind': 'const', 'value': 1.0, 'sym': False})
+
+
 INITS = {
     'metrohast_norm1d': [50., 12.5], 'mcmc_prob2': [0.], 'mcmc_prob3': [5.],
     'mcmc_prob4a': [0., 1.], 'mcmc_prob4b': [5., 5.], 'mcmc_prob6': [0., 1.],
     'gibbs_norm2d': [0., 1.], 'diag10': [0.] * 10, 'gibbs8': [0.] * 8,
     'gibbs_sweep2': [0., 0.],
-    'gmm2': [0., 0.],
+    'gmm2': [0., 0.], 'covrw2': [0., 0.], 'covrw5': [0.] * 5,
 }
 
 WORKLOADS = {
@@ -175,6 +204,7 @@ WORKLOADS = {
     'gibbs_norm2d': spec_gibbs_norm2d, 'diag10': spec_diag10,
     'gibbs8': spec_gibbs8, 'gmm2': spec_gmm2,
     'gibbs_sweep2': spec_gibbs_sweep2,
+    'covrw2': spec_covrw2, 'covrw5': spec_covrw5,
 }
 
 

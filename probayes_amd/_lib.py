@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PBHIP_LIB', os.path.join(_HERE, 'libpbhip.so'))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_DIM = 32
 
 # enums (pbhip.h)
@@ -52,7 +52,7 @@ class PbhProposal(ctypes.Structure):
   _fields_ = [
       ('kind', ctypes.c_int32), ('loc', _dp), ('scale', _dp),
       ('order', _ip), ('delta', ctypes.c_double), ('lengths', _dp),
-      ('delta_vec', _dp),
+      ('delta_vec', _dp), ('tfun', _dp),
   ]
 
 

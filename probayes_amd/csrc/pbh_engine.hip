@@ -396,6 +396,12 @@ int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
     default:
       return fail(PBH_ERR_ARG, "bad proposal kind %d (GIBBS: pbh_set_gibbs)", p->kind);
   }
+  size_t otf = 0;
+  if (p->tfun) {
+    for (int i = 0; i < d * d; ++i)
+      if (!std::isfinite(p->tfun[i])) return fail(PBH_ERR_ARG, "tfun must be finite");
+    otf = pack(blk, p->tfun, (size_t)d * d);
+  }
   HIP_TRY(hipSetDevice(e->device));
   int rc = upload(e->dprop, blk, e->stream);
   if (rc) return rc;
@@ -404,6 +410,8 @@ int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
   k.ploc = e->dprop + oloc; k.pscl = e->dprop + oscl;
   k.plen = e->dprop + olen; k.pdel = e->dprop + odel;
   k.sdelta = p->delta;
+  k.ptf = p->tfun ? e->dprop + otf : nullptr;
+  k.has_tfun = p->tfun ? 1 : 0;
   e->has_prop = true;
   e->has_gibbs = false;
   return PBH_OK;

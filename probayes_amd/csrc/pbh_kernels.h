@@ -26,6 +26,8 @@ struct KArgs {
   int32_t prop;
   const double *ploc, *pscl, *plen, *pdel;
   double sdelta;
+  const double *ptf;  // covariance RW: delta' = ptf[d][d] . delta (rf.py:340-354)
+  int32_t has_tfun;
   // ---- gibbs ----
   const double *gmean, *gcoef, *gstdv, *gcdf;
   int32_t tsteps;

@@ -43,6 +43,26 @@ __device__ __forceinline__ double uni(double v) {
   return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
 }
 
+// Covariance-matrix random walk (rf.py:340-354): delta' = tfun() . delta
+// with the Cholesky factor RF.set_tran(ndarray) installs (rf.py:210-220).
+// Row k sums tfun[k][j] * delta[j] in j order (the zero half of a triangular
+// factor adds exact zeros); the factor is read with wave-uniform scalar
+// loads.  d^2 FMAs per chain-step on the VALU: the per-chain (d x d)(d)
+// product has no cross-chain reuse for the matrix cores at d <= 32.
+template <int D>
+__device__ __forceinline__ void apply_tfun(const double *tf, double (&dl)[D]) {
+  double out[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    double acc = cld(tf, k * D) * dl[0];
+#pragma unroll
+    for (int j = 1; j < D; ++j) acc = acc + cld(tf, k * D + j) * dl[j];
+    out[k] = acc;
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) dl[k] = out[k];
+}
+
 // prob.py:354-357: the mvn density is evaluated at the values reversed and,
 // for d > 2, rotated by one: [x_{d-2}, ..., x_0, x_{d-1}] (App. A-4).
 template <int D>
@@ -488,6 +508,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 #pragma unroll
         for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * cld(a.plen, k);
       }
+      if (a.has_tfun) apply_tfun<D>(a.ptf, dl);   // wave-uniform
 #pragma unroll
       for (int k = 0; k < D; ++k)
         xp[k] = ((a.ufun >> k) & 1u)
@@ -1683,7 +1704,7 @@ void launch_mh_pair(const KArgs &a, hipStream_t st) {
 // Gaussian delta, no ufun / prior, symmetric tran or metropolis, debug off.
 inline bool pair_form(const KArgs &a) {
   return a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS &&
-         a.ufun == 0 && !a.has_prior && !a.debug &&
+         a.ufun == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
          (a.scores == PBH_SCORES_METROPOLIS ||
           (a.scores == PBH_SCORES_HASTINGS && a.tran_sym &&
            a.tran_kind == PBH_TRAN_CONST));
@@ -1693,7 +1714,7 @@ inline bool pair_form(const KArgs &a) {
 // ufun / prior / debug records.
 inline bool gmm_pair_form(const KArgs &a) {
   return a.rng == PBH_RNG_PHILOX && a.simple_acc && a.pair_ok && a.ufun == 0 &&
-         !a.has_prior && !a.debug;
+         !a.has_prior && !a.debug && !a.has_tfun;
 }
 
 template <int D>

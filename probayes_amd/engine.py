@@ -158,6 +158,8 @@ class Engine:
       q.lengths = _dp(arr(p['lengths']))
     elif p['kind'] == 'uniform':
       q.delta_vec = _dp(arr(p['delta']))
+    if p.get('tfun') is not None:
+      q.tfun = _dp(arr(np.ascontiguousarray(p['tfun'], np.float64)))
     _lib.call('pbh_set_proposal', self._h, _c.byref(q))
 
   def _set_gibbs(self):

@@ -122,9 +122,21 @@ class RF:
 
   def set_tran(self, tran=None, *args, **kwds):
     """rf.py:169-239: a callable, a (forward, reverse) tuple, a scipy
-    multivariate_normal (CondCov Gibbs, tsteps=) or an RF to delegate to."""
+    multivariate_normal (CondCov Gibbs, tsteps=), an RF to delegate to, or a
+    covariance matrix: a square array sets its Cholesky factor as the tfun
+    (rf.py:210-220) that multiplies every delta (rf.py:340-354)."""
     kwds = dict(kwds)
     self.tran = (tran, args, kwds)
+    if isinstance(tran, np.ndarray):
+      d = len(self.rvs)
+      if tran.ndim != 2 or tran.shape != (d, d):
+        raise AssertionError('Non-callable non-scalar tran objects must be a '
+                             'square 2D Numpy array of size corresponding to '
+                             'number of variables {}'.format(d))
+      if kwds.get('tsteps'):
+        raise AssertionError('Setting tsteps not supported for covariance '
+                             'transitions')
+      self.set_tfun(np.linalg.cholesky(tran))
 
   def set_delta(self, delta=None, *args, **kwds):
     """field.py:220-317: scalar in a tuple (spherical), in a list (uniform
@@ -134,7 +146,23 @@ class RF:
     self.delta_kwds = dict(kwds)
 
   def set_tfun(self, tfun=None, *args, **kwds):
-    self.tfun = (tfun, args, kwds)
+    """rf.py:247-304.  A non-callable tfun is a triangular (LU) factor."""
+    if isinstance(tfun, np.ndarray):
+      d = len(self.rvs)
+      if tfun.ndim != 2 or tfun.shape != (d, d) or not (
+          np.allclose(tfun, np.tril(tfun)) or np.allclose(tfun, np.triu(tfun))):
+        raise AssertionError('Non-callable tran objects must be a triangular '
+                             '2D Numpy array of size corresponding to number '
+                             'of variables {}'.format(d))
+      tfun = np.array(tfun, dtype=np.float64)
+    self.tfun = None if tfun is None else (tfun, args, kwds)
+
+  @property
+  def lud(self):
+    """The triangular tfun factor, or None (rf.py:347-349)."""
+    if self.tfun is not None and isinstance(self.tfun[0], np.ndarray):
+      return self.tfun[0]
+    return None
 
   def __repr__(self):
     return '&'.join(self.keylist)

@@ -76,11 +76,34 @@ class SP:
   def set_prob(self, prob=None, *args, **kwds):
     self._prob = (prob, args, dict(kwds))
 
+  def _subfield(self, spec):
+    """dependence.py:316-326: an RF of this process or its subfield name
+    ('leafs' for a one-field SP; 'leafs' / 'roots' for SP(leafs, roots))."""
+    if isinstance(spec, RF):
+      return spec
+    if isinstance(spec, str):
+      fields = {'leafs': self.roots} if self.leafs is None else \
+          {'leafs': self.leafs, 'roots': self.roots}
+      if spec not in fields:
+        raise AssertionError('{} absent from {}'.format(spec, self.roots))
+      return fields[spec]
+    return None
+
   def set_tran(self, tran=None, *args, **kwds):
-    self._tran = tran if isinstance(tran, RF) else (tran, args, dict(kwds))
+    """sd.py:97-105.  An RF (or its subfield name) lends its tran and tfun;
+    the process's own _sym_tran is then left unset, so hastings takes the
+    reverse branch with r = q (sd.py:276-277, rf.py:536)."""
+    if isinstance(tran, np.ndarray):
+      # dependence.py:320 compares the array with the subfields and raises
+      raise ValueError('The truth value of an array with more than one '
+                       'element is ambiguous. Use a.any() or a.all()')
+    sub = self._subfield(tran)
+    self._tran = sub if sub is not None else (tran, args, dict(kwds))
 
   def set_delta(self, delta=None, *args, **kwds):
-    self._delta = delta if isinstance(delta, RF) else (delta, args, dict(kwds))
+    """dependence.py:329-339: an RF (or its subfield name) lends its delta."""
+    sub = self._subfield(delta)
+    self._delta = sub if sub is not None else (delta, args, dict(kwds))
 
   def set_tfun(self, tfun=None, *args, **kwds):
     self._tfun = tfun
@@ -217,7 +240,11 @@ class SP:
       return make_spec(d, target, proposal, scores='gibbs', pscale=pscale,
                        prior=prior, ufun=ufun, names=names)
     proposal = self._lower_delta(rvs, names)
-    tran_spec = self._lower_tran(tran, names, scores)
+    lud = self._tran.lud if isinstance(self._tran, RF) else None
+    if lud is not None:
+      proposal['tfun'] = lud
+    tran_spec = self._lower_tran(tran, names, scores,
+                                 via_rf=isinstance(self._tran, RF))
     return make_spec(d, target, proposal, scores=scores, pscale=pscale,
                      tran=tran_spec, prior=prior, ufun=ufun, names=names)
 
@@ -247,12 +274,22 @@ class SP:
       return L.trace_delta(delta, names)
     raise L.NotLowerable('delta {} has no kernel'.format(delta))
 
-  def _lower_tran(self, tran, names, scores):
+  def _lower_tran(self, tran, names, scores, via_rf=False):
     if scores == 'metropolis':
       return None
     if not tran or tran[0] is None:
       raise L.NotLowerable('hastings scores need set_tran()')
     t = tran[0]
+    if isinstance(t, np.ndarray):
+      # a covariance tran is not callable: eval_tran returns the default
+      # conditional of the RF's pscale (rf.py:20, 510-511)
+      rf = self._tran
+      return {'kind': 'const', 'sym': not via_rf,
+              'value': 0. if any(is_log(v.pscale) for v in rf.rvs) else 1.}
+    if via_rf:
+      form = L.trace_tran(t[0] if isinstance(t, tuple) else t, names)
+      form['sym'] = False
+      return form
     if isinstance(t, tuple):
       form = L.trace_tran(t[0], names)
       form['sym'] = False

@@ -16,6 +16,8 @@ encodes the closed set of model forms the engine lowers:
   proposal kind gauss   callable Delta(norm.rvs(loc, scale)) per dim
                 sphere  tuple delta (field.py:509-531)
                 uniform list delta (variable.py:625-633)
+                (any of the three may carry tfun [d, d]: the covariance
+                random walk delta' = tfun . delta, rf.py:210-220, 340-354)
                 gibbs   CondCov conditional sampling (cond_cov.py:22-65)
   tran     kind const (value) | gauss_pdf (scale, offset, order); sym flag
   scores        hastings | metropolis | gibbs (sp_utils.py:87-91)
@@ -103,6 +105,13 @@ def make_spec(dim, target, proposal, scores='hastings', pscale=None,
     proposal['lo'] = _vec(proposal['lo'], d, 'lo')
     proposal['hi'] = _vec(proposal['hi'], d, 'hi')
     proposal['tsteps'] = int(proposal.get('tsteps', 1))
+  if proposal.get('tfun') is not None:
+    if pk == 'gibbs':
+      raise ValueError('tfun applies to MH deltas, not to gibbs')
+    tf = np.array(proposal['tfun'], dtype=np.float64)
+    if tf.shape != (d, d) or not np.all(np.isfinite(tf)):
+      raise ValueError('tfun must be a finite [{0}, {0}] matrix'.format(d))
+    proposal['tfun'] = tf
   if tran is None:
     tran = {'kind': 'const', 'value': 1.0, 'sym': True}
   tran = dict(tran)

@@ -251,3 +251,67 @@ def gibbs_sweep2(pb, params):
 
 
 WORKLOADS['gibbs_sweep2'] = (gibbs_sweep2, {}, 16, 256, 11000)
+
+
+# ----------------------------------------------------------------------------
+# Covariance-matrix random walk: RF.set_tran(ndarray)
+# sets the Cholesky factor as the RF's tfun (rf.py:210-220) and RF.eval_delta
+# multiplies every base delta by it (rf.py:340-354); the SP reaches the RF's
+# tran and delta through its subfield name (sd.py:97-105, dependence.py:316-
+# 339), which is the route that runs (SP.set_tran(ndarray) itself fails in
+# leafs_roots on the array comparison).
+# ----------------------------------------------------------------------------
+def covrw2(pb, params):
+  """examples/cov/multinorm_rw.py:6-15 model (mvn target at the permuted
+  vector, App. A-4) with a covariance RW proposal: callable N(0, 0.5^2)
+  Delta times chol(cov)."""
+  lims = (-10., 10.)
+  means = [0.5, -0.5]
+  covar = np.array([[1.5, -1.0], [-1.0, 2.]])
+  x = pb.RV('x', vtype=float, vset=lims)
+  y = pb.RV('y', vtype=float, vset=lims)
+  xy = x & y
+  xy.set_tran(covar)
+  step = params['step']
+  xy.set_delta(lambda: xy.Delta(x=scipy.stats.norm.rvs(scale=step),
+                                y=scipy.stats.norm.rvs(scale=step)))
+  process = pb.SP(xy)
+  process.set_prob(scipy.stats.multivariate_normal, means, covar)
+  process.set_tran('leafs')
+  process.set_delta('leafs')
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {'x': 0., 'y': 0.}, None, {}, ['x', 'y']
+
+
+def covrw5(pb, params):
+  """5-dim diagonal-Gaussian target (the H3 form at d = 5) under a
+  covariance RW proposal from a spherical tuple delta (field.py:509-531)
+  times chol(cov) (rf.py:340-354)."""
+  mus, sigmas, cov = params['mu'], params['sigma'], params['cov']
+  keys = ['x{}'.format(i) for i in range(len(mus))]
+  xs = [pb.RV(k, vtype=float, vset=(-10., 10.)) for k in keys]
+  rf = pb.RF(*xs)
+  rf.set_tran(cov)
+  rf.set_delta((params['step'],))
+  process = pb.SP(rf)
+  def lp(**kw):
+    return sum(scipy.stats.norm.logpdf(kw[k], mus[i], sigmas[i])
+               for i, k in enumerate(keys))
+  process.set_prob(lp, pscale='log')
+  process.set_tran('leafs')
+  process.set_delta('leafs')
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, {k: 0. for k in keys}, None, {}, keys
+
+
+def _covrw5_params():
+  rs = np.random.RandomState(55)
+  A = rs.normal(size=(5, 5))
+  return {'mu': np.linspace(-1., 1., 5), 'sigma': np.linspace(0.5, 2., 5),
+          'cov': A.dot(A.T) / 5 + 0.25 * np.eye(5), 'step': 0.6}
+
+
+WORKLOADS['covrw2'] = (covrw2, {'step': 0.5}, 16, 256, 12000)
+WORKLOADS['covrw5'] = (covrw5, _covrw5_params(), 16, 256, 13000)

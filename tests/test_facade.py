@@ -128,3 +128,36 @@ def test_batched_philox_sampler_posterior(rng):
   x = g['param_x_obs']
   assert abs(np.mean(mus) - np.mean(x)) < 0.5
   assert abs(np.median(sig) - np.std(x)) < 1.5
+
+
+def test_covariance_tran_routes_like_the_reference():
+  """rf.py:210-220 (cholesky tfun), dependence.py:316-326 (subfield names),
+  sd.py:97-105 (SP.set_tran(ndarray) fails in leafs_roots)."""
+  cov = np.array([[1.5, -1.0], [-1.0, 2.]])
+  x = pb.RV('x', vtype=float, vset=(-10., 10.))
+  y = pb.RV('y', vtype=float, vset=(-10., 10.))
+  xy = x & y
+  xy.set_tran(cov)
+  np.testing.assert_array_equal(xy.lud, np.linalg.cholesky(cov))
+  process = pb.SP(xy)
+  with pytest.raises(ValueError):
+    process.set_tran(cov)
+  with pytest.raises(AssertionError):
+    process.set_tran('roots')              # a one-field SP has only 'leafs'
+  with pytest.raises(AssertionError):
+    xy.set_tran(np.eye(3))
+  with pytest.raises(AssertionError):
+    xy.set_tfun(np.array([[1., 2.], [3., 4.]]))   # not triangular
+  xy.set_delta([0.5])
+  import scipy.stats
+  def lp(**kw):
+    return scipy.stats.norm.logpdf(kw['x'], 0., 1.) + \
+        scipy.stats.norm.logpdf(kw['y'], 0., 2.)
+  process.set_prob(lp, pscale='log')
+  process.set_tran('leafs')
+  process.set_delta('leafs')
+  process.set_scores('hastings')
+  spec = process.lower()
+  np.testing.assert_array_equal(spec['proposal']['tfun'], np.linalg.cholesky(cov))
+  assert spec['proposal']['kind'] == 'uniform'
+  assert spec['tran'] == {'kind': 'const', 'value': 1.0, 'sym': False}
