@@ -200,6 +200,19 @@ int pbh_rccl_allgather_moments(pbh_engine *eng, double *out);
 int pbh_rccl_allreduce_max(pbh_engine *eng, double *value);
 int pbh_rccl_destroy(pbh_engine *eng);
 
+/* ---- likelihoods (likelihoods.py) --------------------------------------- */
+/* bool_perm_freq (likelihoods.py:45-101): counts[2^cols] (C order: the first
+ * column is the most significant index bit, each dimension ordered [False,
+ * True]) of the boolean row patterns of bool2d [rows][cols] (one byte per
+ * element, non-zero = True).  1 <= cols <= 26; rows = 0 gives zero counts.
+ * Host buffers.  The kernel runs `reps` >= 1 times on device-resident input
+ * after one untimed warm-up launch (counts of the last run are returned);
+ * *kernel_ms (may be NULL) receives
+ * the average kernel time from HIP events.                                  */
+int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
+                       const uint8_t *bool2d, int64_t *counts, int32_t reps,
+                       double *kernel_ms);
+
 /* ---- diagnostics -------------------------------------------------------- */
 /* Evaluates the production-mode acceptance filter and the exact ratio form
  * (sp_utils.py:40-64) on device for n triples (lp, lp', t = u01(t0, t1)).

@@ -14,3 +14,5 @@ from probayes_amd.sp import SP  # noqa: F401,E402
 from probayes_amd.pd import PD  # noqa: F401,E402
 from probayes_amd.lower import NotLowerable  # noqa: F401,E402
 from probayes_amd import models  # noqa: F401,E402
+from probayes_amd import likelihoods  # noqa: F401,E402
+from probayes_amd.likelihoods import bool_perm_freq  # noqa: F401,E402

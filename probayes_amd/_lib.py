@@ -100,6 +100,12 @@ SIGNATURES = {
                                         _u32p, _u32p, ctypes.c_int32, _u8p]),
     'pbh_check_normals': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _u32p,
                                          _dp, _dp]),
+    'pbh_bool_perm_freq': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64,
+                                          ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_uint8),
+                                          ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_double)]),
 }
 
 

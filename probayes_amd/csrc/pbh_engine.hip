@@ -947,6 +947,66 @@ int pbh_check_accept(int device, int64_t n, const double *lp,
   return PBH_OK;
 }
 
+int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
+                       const uint8_t *bool2d, int64_t *counts, int32_t reps,
+                       double *kernel_ms) {
+  if (check_ptr(counts, "counts")) return PBH_ERR_ARG;
+  if (cols < 1 || cols > pbh::bool_perm_max_cols())
+    return fail(PBH_ERR_ARG, "cols must be in 1..%d, got %d",
+                pbh::bool_perm_max_cols(), cols);
+  if (rows < 0) return fail(PBH_ERR_ARG, "rows must be >= 0");
+  if (rows > 0 && !bool2d) return fail(PBH_ERR_ARG, "bool2d must not be NULL");
+  if (reps < 1) return fail(PBH_ERR_ARG, "reps must be >= 1");
+  const int64_t nbins = (int64_t)1 << cols;
+  if (kernel_ms) *kernel_ms = 0.;
+  if (rows == 0) {
+    std::memset(counts, 0, nbins * sizeof(int64_t));
+    return PBH_OK;
+  }
+  HIP_TRY(hipSetDevice(device));
+  int n_cu = 0;
+  HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
+  uint8_t *din = nullptr;
+  unsigned long long *dcnt = nullptr, *dscr = nullptr;
+  int rc = dalloc(din, rows * cols);
+  if (!rc) rc = dalloc(dcnt, nbins);
+  if (!rc) rc = dalloc(dscr, pbh::bool_perm_scratch_words(n_cu));
+  hipError_t err = hipSuccess;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double total = 0.;
+  if (!rc) {
+    err = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (err == hipSuccess) err = hipEventCreate(&e0);
+    if (err == hipSuccess) err = hipEventCreate(&e1);
+    if (err == hipSuccess)
+      err = hipMemcpy(din, bool2d, (size_t)(rows * cols), hipMemcpyHostToDevice);
+    // r = 0 is an untimed warm-up launch (the code object loads lazily on
+    // the first launch); the average is over the `reps` timed launches
+    for (int r = 0; r <= reps && err == hipSuccess; ++r) {
+      err = hipMemsetAsync(dcnt, 0, nbins * sizeof(unsigned long long), st);
+      if (err == hipSuccess) err = hipEventRecord(e0, st);
+      if (err == hipSuccess) err = pbh::launch_bool_perm_freq(din, rows, cols, dcnt, dscr, n_cu, st);
+      if (err == hipSuccess) err = hipEventRecord(e1, st);
+      if (err == hipSuccess) err = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+      if (r > 0) total += ms;
+    }
+    if (err == hipSuccess)
+      err = hipMemcpy(counts, dcnt, nbins * sizeof(int64_t), hipMemcpyDeviceToHost);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  dfree(din); dfree(dcnt); dfree(dscr);
+  if (rc) return rc;
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_bool_perm_freq: %s", hipGetErrorString(err));
+  if (kernel_ms) *kernel_ms = total / reps;
+  return PBH_OK;
+}
+
 int pbh_check_normals(int device, int64_t n, const uint32_t *words,
                       double *fast, double *ref) {
   if (check_ptr(words, "words") || check_ptr(fast, "fast") || check_ptr(ref, "ref"))

@@ -94,6 +94,14 @@ hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
 bool mh_dim_supported(int d);
 hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
                                 double *ref);
+// bool_perm_freq histogram (pbh_likelihoods.hip); counts must be zeroed,
+// scratch holds bool_perm_scratch_words(n_cu) u64 partials.
+int bool_perm_max_cols();
+int64_t bool_perm_scratch_words(int n_cu);
+hipError_t launch_bool_perm_freq(const uint8_t *in, int64_t rows, int cols,
+                                 unsigned long long *counts,
+                                 unsigned long long *scratch, int n_cu,
+                                 hipStream_t s);
 hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
                                const uint32_t *t0, const uint32_t *t1,
                                int32_t lin, double log_npi, uint8_t *out);

@@ -7,7 +7,12 @@
   cfg5  3-component 2-D GMM, 32 768 chains (the per-GPU share of 262 144),
         2 000 steps, ESS/s (initial-positive-sequence ESS, min over dims,
         summed over chains, / kernel wall time)
-One JSON line per workload.  Kernel time from the engine's HIP events.
+  lik   likelihoods.py bool_perm_freq: 2^28 rows x 2 columns (naive-Bayes
+        table shape of examples/naive), HBM read stream
+One JSON line per workload.  Kernel time from HIP events.  Each line carries
+a roofline object (algorithmic HBM bytes / kernel time against 8 TB/s) and a
+cpu_baseline: the oracle (the NumPy restatement of the reference, bit-exact
+on the golden vectors) timed on a bounded sample on one host core.
 """
 import json
 import os
@@ -40,6 +45,35 @@ def ess_ips(x):
   return t / np.maximum(1.0 + 2.0 * s, 1e-12)
 
 
+PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def roofline(bytes_per_unit, units, ms, kernel):
+  gbs = bytes_per_unit * units / (ms / 1e3) / 1e9
+  return {'bound': 'hbm', 'achieved': gbs, 'peak': PEAK_GBS, 'unit': 'GB/s',
+          'frac': gbs / PEAK_GBS, 'traffic': None,
+          'bytes_per_unit': bytes_per_unit, 'kernel': kernel}
+
+
+def cpu_chain_rate(name, n, t, budget_s):
+  """Oracle chain-steps (or coordinate steps) per second on one core,
+  including its legacy-MT19937 stream generation."""
+  spec = oracle.golden_spec(name)
+  run_ = oracle.run_gibbs if spec['scores'] == 'gibbs' else oracle.run_mh
+  done, reps, t0 = 0, 0, time.perf_counter()
+  while time.perf_counter() - t0 < budget_s:
+    seeds = np.arange(reps * n, (reps + 1) * n)
+    run_(spec, oracle.workloads.golden_init(name, n),
+         oracle.legacy_streams(spec, seeds, t))
+    done += n * t
+    reps += 1
+  el = time.perf_counter() - t0
+  return {'value': done / el, 'unit': 'chain-steps/s', 'cores': 1,
+          'kind': 'port',
+          'sample': '{} chains x {} steps x {} reps of {} through the oracle '
+                    'incl. per-chain RandomState streams'.format(n, t, reps, name)}
+
+
 def run(name, n, steps, rng='philox', spl=0, trace=True):
   spec = oracle.golden_spec(name)
   eng = Engine(spec)
@@ -57,15 +91,50 @@ def run(name, n, steps, rng='philox', spl=0, trace=True):
   return eng, out
 
 
+def bench_bool_perm_freq(cpu, budget_s):
+  """likelihoods.py:45-101 at 2^28 rows x 2 columns, input resident in HBM;
+  the kernel reads every byte once (cols bytes per row)."""
+  from probayes_amd.likelihoods import bool_counts
+  from oracle.likelihoods import bool_perm_counts
+  rows, cols = 1 << 28, 2
+  a = np.random.RandomState(3).randint(0, 2, size=(rows, cols),
+                                       dtype=np.uint8).view(bool)
+  counts, ms = bool_counts(a, reps=5)
+  assert counts.sum() == rows
+  o = {'workload': 'bool_perm_freq', 'rows': rows, 'cols': cols,
+       'rows_per_s': rows / (ms / 1e3), 'kernel_ms': ms,
+       'roofline': roofline(cols, rows, ms,
+                           'bool_perm_direct<2> + bool_perm_reduce'),
+       'config': 'likelihoods.py bool_perm_freq, naive-Bayes table shape'}
+  if cpu:
+    n = 1 << 22
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+      bool_perm_counts(a[:n])
+      done += n
+    el = time.perf_counter() - t0
+    o['cpu_baseline'] = {'value': done / el, 'unit': 'rows/s', 'cores': 1,
+                         'kind': 'port',
+                         'sample': '{} rows x {} cols through '
+                                   'oracle.bool_perm_counts (np.bincount); '
+                                   'the reference loops over rows in '
+                                   'Python'.format(n, cols)}
+  return o
+
+
 def main():
   import argparse
   ap = argparse.ArgumentParser()
-  ap.add_argument('--only', default='cfg1,cfg3,cfg5',
-                  help='comma-separated subset of cfg1,cfg3,cfg5')
+  ap.add_argument('--only', default='cfg1,cfg3,cfg5,lik',
+                  help='comma-separated subset of cfg1,cfg3,cfg5,lik')
+  ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--cpu-budget', type=float, default=4.0,
+                  help='seconds of oracle work per cpu_baseline')
   ap.add_argument('--no-trace', action='store_true',
                   help='cfg3 without the trace (arithmetic-only probe)')
   args = ap.parse_args()
   only = args.only.split(',')
+  cpu = not args.no_cpu_baseline
   lines = []
   if 'cfg1' in only:
     eng, o = run('metrohast_norm1d', 128, 2000)
@@ -73,13 +142,26 @@ def main():
     lines.append(dict(o, config='cfg1 (128 chains)'))
     eng, o = run('metrohast_norm1d', 65536, 1000)
     eng.close()
+    o['roofline'] = roofline(2 * 8 + 8 + 1 / 8, 65536 * 1000, o['kernel_ms'],
+                             'mh_kernel<2, PHILOX, NORM_IID, SPHERE>')
+    if cpu:
+      o['cpu_baseline'] = cpu_chain_rate('metrohast_norm1d', 256, 8,
+                                         args.cpu_budget)
     lines.append(dict(o, config='cfg1 model at 65536 chains'))
   if 'cfg3' in only:
     eng, o = run('gibbs8', 32768, 8 * 256, trace=not args.no_trace)
     o['coordinate_steps_per_s'] = o.pop('chain_steps_per_s')
     o['hbm_gbs'] = o['coordinate_steps_per_s'] * (8 * 8 + 8 + 1 / 8) / 1e9
     eng.close()
+    o['roofline'] = roofline(8 * 8 + 8 + 1 / 8, 32768 * 8 * 256,
+                             o['kernel_ms'], 'gibbs_fast_kernel<8, 2>')
+    if cpu:
+      o['cpu_baseline'] = dict(cpu_chain_rate('gibbs8', 256, 16,
+                                              args.cpu_budget),
+                               unit='coordinate-steps/s')
     lines.append(dict(o, config='cfg3'))
+  if 'lik' in only:
+    lines.append(bench_bool_perm_freq(cpu, args.cpu_budget))
   if 'cfg5' not in only:
     for line in lines:
       print(json.dumps(line), flush=True)
@@ -92,6 +174,10 @@ def main():
   o['ess_min_dim'] = float(min(ess))
   o['ess_per_s'] = o['ess_min_dim'] / (o['kernel_ms'] / 1e3)
   o['ess_host_s'] = time.perf_counter() - t0
+  o['roofline'] = roofline(2 * 8 + 8 + 1 / 8, 32768 * 2000, o['kernel_ms'],
+                           'mh_gmm_lanes_kernel<2, 3, 2>')
+  if cpu:
+    o['cpu_baseline'] = cpu_chain_rate('gmm2', 512, 8, args.cpu_budget)
   lines.append(dict(o, config='cfg5 per-GPU share'))
   for line in lines:
     print(json.dumps(line), flush=True)

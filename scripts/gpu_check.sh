@@ -20,10 +20,10 @@ step bench_xo 120 python bench.py --rng xoshiro --no-cpu-baseline
 step workloads 240 python scripts/bench_workloads.py
 [ -x tools/ubench/isa_cost ] && step isa_cost 120 tools/ubench/isa_cost
 [ -x tools/ubench/store_pattern ] && step store_pattern 120 tools/ubench/store_pattern
-step gibbs_lanes4 120 env PBH_GIBBS_LANES=4 python scripts/bench_workloads.py --only cfg3
-step gibbs_ndtri 120 env PBH_GIBBS_FAST=0 python scripts/bench_workloads.py --only cfg3
-step gibbs_ndtri_valu 120 env PBH_GIBBS_FAST=0 PBH_GIBBS_MFMA=0 python scripts/bench_workloads.py --only cfg3
-step gmm_lanes4 120 env PBH_GMM_LANES=4 python scripts/bench_workloads.py --only cfg5
+step gibbs_lanes4 120 env PBH_GIBBS_LANES=4 python scripts/bench_workloads.py --only cfg3 --no-cpu-baseline
+step gibbs_ndtri 120 env PBH_GIBBS_FAST=0 python scripts/bench_workloads.py --only cfg3 --no-cpu-baseline
+step gibbs_ndtri_valu 120 env PBH_GIBBS_FAST=0 PBH_GIBBS_MFMA=0 python scripts/bench_workloads.py --only cfg3 --no-cpu-baseline
+step gmm_lanes4 120 env PBH_GMM_LANES=4 python scripts/bench_workloads.py --only cfg5 --no-cpu-baseline
 P=$O/prof; mkdir -p $P; cd /tmp
 A="--steps 1000 --warmup 250 --no-cpu-baseline"
 step prof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- python3 $R/bench.py $A
@@ -32,7 +32,9 @@ step prof_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -
 step prof_sq1 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR --output-format csv -d $P/sq1 -o run -- python3 $R/bench.py $A
 step prof_sq2 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d $P/sq2 -o run -- python3 $R/bench.py $A
 step prof_sq3 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_WR GRBM_GUI_ACTIVE --output-format csv -d $P/sq3 -o run -- python3 $R/bench.py $A
-step prof_wl 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/wl -o run -- python3 $R/scripts/bench_workloads.py
-step prof_wl_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/wl_fetch -o run -- python3 $R/scripts/bench_workloads.py --only cfg3
-step prof_wl_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/wl_write -o run -- python3 $R/scripts/bench_workloads.py --only cfg3
+step prof_wl 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/wl -o run -- python3 $R/scripts/bench_workloads.py --no-cpu-baseline
+step prof_wl_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/wl_fetch -o run -- python3 $R/scripts/bench_workloads.py --only cfg3 --no-cpu-baseline
+step prof_wl_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/wl_write -o run -- python3 $R/scripts/bench_workloads.py --only cfg3 --no-cpu-baseline
+step prof_lik_fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/lik_fetch -o run -- python3 $R/scripts/bench_workloads.py --only lik --no-cpu-baseline
+step prof_lik_write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/lik_write -o run -- python3 $R/scripts/bench_workloads.py --only lik --no-cpu-baseline
 echo done
