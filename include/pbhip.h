@@ -160,6 +160,19 @@ int pbh_set_rng(pbh_engine *eng, int32_t mode, uint64_t seed);
  * consumed from the next pbh_run step on.                                   */
 int pbh_upload_replay(pbh_engine *eng, int64_t n_steps, const double *rand);
 int pbh_stream_width(pbh_engine *eng, int32_t *r);
+/* The same streams generated on the device: one NumPy legacy RandomState per
+ * chain (MT19937 seeded as RandomState(seeds[c]), random_sample, polar
+ * legacy gauss with its cached deviate), drawn in the reference's per-step
+ * order.  pbh_legacy_seed seeds the engine's chains;
+ * each pbh_legacy_replay fills the replay stream with the next n_steps rows
+ * of every chain's generator (continuing where the last call stopped) for
+ * the runs from the current step on.  pbh_get_replay copies steps [first,
+ * first + n_steps) of the current stream back: draw < 0 gives every draw in
+ * the pbh_upload_replay layout [n][R][N], draw = j only draw j, [n][N].   */
+int pbh_legacy_seed(pbh_engine *eng, const uint32_t *seeds);
+int pbh_legacy_replay(pbh_engine *eng, int64_t n_steps);
+int pbh_get_replay(pbh_engine *eng, int64_t first, int64_t n_steps,
+                   int32_t draw, double *out);
 
 /* ---- running (SP.walk / sample_generator: sp.py:281-295, sp_utils.py:8-16) */
 /* Device trace ring for the next runs: every thin-th step is recorded.

@@ -78,6 +78,10 @@ SIGNATURES = {
                                    ctypes.c_uint64]),
     'pbh_upload_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _dp]),
     'pbh_stream_width': (ctypes.c_int, [ctypes.c_void_p, _ip]),
+    'pbh_legacy_seed': (ctypes.c_int, [ctypes.c_void_p, _u32p]),
+    'pbh_legacy_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    'pbh_get_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.c_int64, ctypes.c_int32, _dp]),
     'pbh_alloc_trace': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.c_int32, ctypes.c_int32]),
     'pbh_run': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),

@@ -43,6 +43,10 @@ struct pbh_engine {
   int64_t rep_steps = 0, rep_g0 = 0;
   uint32_t *xo = nullptr;      // xoshiro128** states [4][2][n]
   bool xo_seeded = false;
+  // legacy NumPy RandomState per chain (pbh_legacy_seed)
+  uint32_t *mt_key = nullptr;
+  int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
+  double *mt_gauss = nullptr;
   // trace
   int64_t cap = 0;
   int32_t thin = 1, debug = 0;
@@ -202,6 +206,8 @@ int pbh_destroy(pbh_engine *e) {
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
   dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq);
+  dfree(e->mt_key); dfree(e->mt_pos); dfree(e->mt_has); dfree(e->mt_order);
+  dfree(e->mt_gauss);
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
@@ -579,6 +585,99 @@ int pbh_upload_replay(pbh_engine *e, int64_t n_steps, const double *rand) {
   e->k.R = R;
   e->rep_steps = n_steps;
   e->rep_g0 = e->g;
+  return PBH_OK;
+}
+
+int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
+  if (check_ptr(e, "engine") || check_ptr(seeds, "seeds")) return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  const int64_t n = e->n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int rc = dalloc(e->mt_key, (size_t)624 * n);
+  if (!rc) rc = dalloc(e->mt_pos, n);
+  if (!rc) rc = dalloc(e->mt_has, n);
+  if (!rc) rc = dalloc(e->mt_gauss, n);
+  if (rc) return rc;
+  uint32_t *dseeds = nullptr;
+  rc = dalloc(dseeds, n);
+  if (rc) return rc;
+  hipError_t err = hipMemcpy(dseeds, seeds, n * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (err == hipSuccess)
+    err = pbh::launch_legacy_seed(e->mt_key, e->mt_pos, e->mt_gauss, e->mt_has,
+                                  dseeds, n, e->stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+  dfree(dseeds);
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_legacy_seed: %s", hipGetErrorString(err));
+  return PBH_OK;
+}
+
+int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first");
+  int32_t R = 0;
+  int rc = pbh_stream_width(e, &R);
+  if (rc) return rc;
+  if (n_steps < 1) return fail(PBH_ERR_ARG, "n_steps must be >= 1");
+  const int64_t n = e->n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  rc = dalloc(e->rep, (size_t)n_steps * R * n);
+  if (!rc && !e->has_gibbs) {
+    rc = dalloc(e->mt_order, e->d);
+    if (!rc) HIP_TRY(hipMemcpy(e->mt_order, e->draw_order.data(),
+                               e->d * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  if (rc) return rc;
+  pbh::LegacyArgs a{};
+  a.key = e->mt_key; a.pos = e->mt_pos; a.gauss = e->mt_gauss;
+  a.has_gauss = e->mt_has; a.order = e->mt_order; a.out = e->rep;
+  a.n = n; a.n_steps = n_steps; a.step0 = e->g;
+  a.d = e->d; a.R = R; a.gibbs = e->has_gibbs ? 1 : 0;
+  a.normal = (!e->has_gibbs && e->k.prop == PBH_PROP_GAUSS) ? 1 : 0;
+  hipError_t err = pbh::launch_legacy_gen(a, e->stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_legacy_replay: %s", hipGetErrorString(err));
+  e->k.R = R;
+  e->rep_steps = n_steps;
+  e->rep_g0 = e->g;
+  return PBH_OK;
+}
+
+int pbh_get_replay(pbh_engine *e, int64_t first, int64_t n_steps, int32_t draw,
+                   double *out) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  if (!e->rep) return fail(PBH_ERR_STATE, "no replay stream");
+  if (first < 0 || n_steps < 0 || first + n_steps > e->rep_steps)
+    return fail(PBH_ERR_ARG, "rows [%lld, %lld) outside the %lld-row stream",
+                (long long)first, (long long)(first + n_steps),
+                (long long)e->rep_steps);
+  const int R = e->k.R;
+  const int64_t n = e->n;
+  if (draw >= R) return fail(PBH_ERR_ARG, "draw %d >= R = %d", draw, R);
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (draw >= 0) {
+    const int src = draw < (int)e->draw_order.size() ? e->draw_order[draw] : draw;
+    HIP_TRY(hipMemcpy2D(out, n * sizeof(double),
+                        e->rep + (size_t)first * R * n + (size_t)src * n,
+                        (size_t)R * n * sizeof(double), n * sizeof(double),
+                        n_steps, hipMemcpyDeviceToHost));
+    return PBH_OK;
+  }
+  std::vector<double> row((size_t)R * n);
+  for (int64_t t = 0; t < n_steps; ++t) {
+    HIP_TRY(hipMemcpy(row.data(), e->rep + (size_t)(first + t) * R * n,
+                      row.size() * sizeof(double), hipMemcpyDeviceToHost));
+    double *dst = out + (size_t)t * R * n;
+    // undo pbh_upload_replay's reordering: draw j sits in row draw_order[j]
+    for (int j = 0; j < R; ++j) {
+      const int src = j < (int)e->draw_order.size() ? e->draw_order[j] : j;
+      std::memcpy(dst + (size_t)j * n, &row[(size_t)src * n], n * sizeof(double));
+    }
+  }
   return PBH_OK;
 }
 

@@ -94,6 +94,22 @@ hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
 bool mh_dim_supported(int d);
 hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
                                 double *ref);
+// Legacy (NumPy RandomState) stream generation (pbh_legacy.hip).
+struct LegacyArgs {
+  uint32_t *key;        // MT19937 words [624][n]
+  int32_t *pos;         // next word per chain [n]
+  double *gauss;        // cached polar deviate [n]
+  int32_t *has_gauss;   // [n]
+  const int32_t *order; // draw j -> replay row order[j] (MH)
+  double *out;          // replay rows [n_steps][R][n]
+  int64_t n, n_steps, step0;
+  int32_t d, R, gibbs, normal;
+};
+hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
+                              int32_t *has_gauss, const uint32_t *seeds,
+                              int64_t n, hipStream_t s);
+hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s);
+
 // bool_perm_freq histogram (pbh_likelihoods.hip); counts must be zeroed,
 // scratch holds bool_perm_scratch_words(n_cu) u64 partials.
 int bool_perm_max_cols();

@@ -1,0 +1,152 @@
+// pbh_legacy.hip -- the reference's random streams generated on the GPU.
+//
+// The reference draws every random number from NumPy's legacy RandomState
+// (SURVEY.md App. A-7): MT19937 seeded by init_genrand (RandomState(int)),
+// random_sample = (a >> 5, b >> 6) 53-bit doubles, and the polar-method
+// legacy gauss with its cached second deviate.  These kernels restate that
+// generator (numpy 2.2.6 random/src/mt19937 + legacy-distributions.c, the
+// version pinned in SURVEY.md §8c) per chain, one chain per lane, and write
+// the draws in the replay layout [T][R][N] the REPLAY kernels read -- so a
+// full-width reference-identical run needs no host stream generation.
+//
+// State per chain: key[624] in [624][N] (word-major, so lanes of a wave
+// touch neighbouring words while their positions agree), pos, the cached
+// gauss and its flag.  Lanes drift apart (the polar rejection consumes a
+// variable number of words); correctness does not depend on it.
+// Per step the order is the reference's: MH draws d normals (callable
+// Gaussian Delta) or d raw doubles (tuple / list delta), then one double for
+// the threshold; CondCov Gibbs draws one double per updated coordinate of
+// the rf.py:446-452 cycle and pads the row with NaN.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pbh_kernels.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kN = 624, kM = 397;
+constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
+
+__global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *pos,
+                                                      double *gauss, int32_t *has_gauss,
+                                                      const uint32_t *seeds, int64_t n) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  uint32_t s = seeds[c];
+  // mt19937_seed (init_genrand)
+  for (int i = 0; i < kN; ++i) {
+    key[(int64_t)i * n + c] = s;
+    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(i + 1);
+  }
+  pos[c] = kN;
+  gauss[c] = 0.0;
+  has_gauss[c] = 0;
+}
+
+struct Mt {
+  uint32_t *key;
+  int64_t n, c;
+  int pos;
+
+  __device__ __forceinline__ uint32_t &k(int i) { return key[(int64_t)i * n + c]; }
+
+  // mt19937_gen: the reference order (later words read updated ones)
+  __device__ void twist() {
+    uint32_t cur = k(0);
+    for (int i = 0; i < kN - 1; ++i) {
+      const uint32_t nxt = k(i + 1);
+      const uint32_t y = (cur & kUpper) | (nxt & kLower);
+      const int j = i < kN - kM ? i + kM : i + kM - kN;
+      k(i) = k(j) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+      cur = nxt;
+    }
+    const uint32_t y = (cur & kUpper) | (k(0) & kLower);
+    k(kN - 1) = k(kM - 1) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    pos = 0;
+  }
+
+  __device__ __forceinline__ uint32_t next32() {
+    if (pos == kN) twist();
+    uint32_t y = k(pos++);
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  // legacy_double / random_sample
+  __device__ __forceinline__ double next_double() {
+    const int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+};
+
+// legacy_gauss: polar method, second deviate cached across calls
+__device__ __forceinline__ double legacy_gauss(Mt &m, double &gauss, int &has) {
+  if (has) {
+    const double t = gauss;
+    has = 0;
+    gauss = 0.0;
+    return t;
+  }
+  double x1, x2, r2;
+  do {
+    x1 = 2.0 * m.next_double() - 1.0;
+    x2 = 2.0 * m.next_double() - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+  } while (r2 >= 1.0 || r2 == 0.0);
+  const double f = sqrt(-2.0 * log(r2) / r2);
+  gauss = f * x1;
+  has = 1;
+  return f * x2;
+}
+
+__global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  Mt m{a.key, a.n, c, a.pos[c]};
+  double gauss = a.gauss[c];
+  int has = a.has_gauss[c];
+  const int64_t rowlen = (int64_t)a.R * a.n;
+  for (int64_t t = 0; t < a.n_steps; ++t) {
+    double *row = a.out + t * rowlen + c;
+    if (a.gibbs) {
+      // rf.py:446-452: block (step0 + t) mod ceil(d / tsteps) of the cycle
+      const int64_t nblk = (a.d + a.R - 1) / a.R;
+      const int cm = (int)(((a.step0 + t) % nblk) * a.R);
+      const int cnt = (cm + a.R < a.d ? cm + a.R : a.d) - cm;
+      for (int j = 0; j < a.R; ++j)
+        row[(int64_t)j * a.n] = j < cnt ? m.next_double() : __builtin_nan("");
+      continue;
+    }
+    for (int j = 0; j < a.d; ++j) {
+      const double v = a.normal ? legacy_gauss(m, gauss, has) : m.next_double();
+      row[(int64_t)a.order[j] * a.n] = v;    // draw j feeds dim order[j]
+    }
+    row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
+  }
+  a.pos[c] = m.pos;
+  a.gauss[c] = gauss;
+  a.has_gauss[c] = has;
+}
+
+}  // namespace
+
+hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
+                              int32_t *has_gauss, const uint32_t *seeds,
+                              int64_t n, hipStream_t s) {
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  hipLaunchKernelGGL(mt_seed_kernel, grid, block, 0, s, key, pos, gauss,
+                     has_gauss, seeds, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
+  hipLaunchKernelGGL(legacy_gen_kernel, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace pbh

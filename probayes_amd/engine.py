@@ -198,6 +198,31 @@ class Engine:
                        .format(streams.shape, self.stream_width(), self.n))
     _lib.call('pbh_upload_replay', self._h, _c.c_int64(T), _dp(streams))
 
+  def seed_legacy(self, seeds):
+    """One NumPy legacy RandomState(seeds[c]) per chain, on the device."""
+    seeds = np.ascontiguousarray(np.asarray(seeds).reshape(-1), dtype=np.int64)
+    if seeds.size != self.n:
+      raise ValueError('need {} seeds, got {}'.format(self.n, seeds.size))
+    if np.any(seeds < 0) or np.any(seeds > 0xFFFFFFFF):
+      raise ValueError('Seed must be between 0 and 2**32 - 1')
+    s32 = np.ascontiguousarray(seeds.astype(np.uint32))
+    _lib.call('pbh_legacy_seed', self._h,
+              s32.ctypes.data_as(_c.POINTER(_c.c_uint32)))
+
+  def legacy_replay(self, n_steps):
+    """Fills the replay stream with the next n_steps rows of every chain's
+    device RandomState (the reference's per-step draw order)."""
+    _lib.call('pbh_legacy_replay', self._h, _c.c_int64(int(n_steps)))
+
+  def get_replay(self, first, n_steps, draw=-1):
+    """Rows of the current replay stream: [n, R, N], or [n, N] of one draw."""
+    r = self.stream_width()
+    shape = (n_steps, r, self.n) if draw < 0 else (n_steps, self.n)
+    out = np.empty(shape, np.float64)
+    _lib.call('pbh_get_replay', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(n_steps)), int(draw), _dp(out))
+    return out
+
   # ---- running -----------------------------------------------------------
   def alloc_trace(self, capacity, thin=1, debug=False):
     _lib.call('pbh_alloc_trace', self._h, _c.c_int64(int(capacity)),

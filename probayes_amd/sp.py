@@ -438,12 +438,22 @@ class Sampler:
         seeds = None if self.seeds is None else np.asarray(self.seeds)
         if seeds is None and self.batched:
           raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
-        streams = replay.legacy_streams(self.spec, self.stop, seeds)
         eng.set_rng('replay')
-        eng.upload_replay(streams)
-        if self.spec['proposal']['kind'] != 'gibbs':
-          th = streams[:, -1, :].T
-          self.thresholds = th[:, self.thin - 1::self.thin]
+        if seeds is None:
+          # one chain on NumPy's GLOBAL stream: drawn on the host so that the
+          # global state advances exactly as the reference leaves it
+          streams = replay.legacy_streams(self.spec, self.stop, seeds)
+          eng.upload_replay(streams)
+          th = streams[:, -1, :] if self.spec['proposal']['kind'] != 'gibbs' \
+              else None
+        else:
+          # RandomState(seeds[c]) per chain, generated on the device
+          eng.seed_legacy(seeds)
+          eng.legacy_replay(self.stop)
+          th = eng.get_replay(0, self.stop, eng.stream_width() - 1) \
+              if self.spec['proposal']['kind'] != 'gibbs' else None
+        if th is not None:
+          self.thresholds = th.T[:, self.thin - 1::self.thin]
       else:
         eng.set_rng(self.rng, self.seed)
       eng.alloc_trace(self.stop // self.thin, self.thin, debug=self.debug)

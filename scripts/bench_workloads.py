@@ -9,6 +9,9 @@
         summed over chains, / kernel wall time)
   lik   likelihoods.py bool_perm_freq: 2^28 rows x 2 columns (naive-Bayes
         table shape of examples/naive), HBM read stream
+  legacy  cfg2 in the reference-identical REPLAY mode: the per-chain NumPy
+        RandomState streams generated on the device, then the reference-
+        arithmetic kernel over them (65 536 chains x 250 steps)
 One JSON line per workload.  Kernel time from HIP events.  Each line carries
 a roofline object (algorithmic HBM bytes / kernel time against 8 TB/s) and a
 cpu_baseline: the oracle (the NumPy restatement of the reference, bit-exact
@@ -122,11 +125,37 @@ def bench_bool_perm_freq(cpu, budget_s):
   return o
 
 
+def bench_legacy_replay():
+  """cfg2 reference-identical: device RandomState streams + REPLAY kernel."""
+  spec = oracle.golden_spec('diag10')
+  n, t = 65536, 250
+  eng = Engine(spec)
+  eng.init_chains(np.zeros((n, 10)))
+  eng.set_rng('replay')
+  eng.seed_legacy(np.arange(n))
+  eng.legacy_replay(8)
+  eng.run(8)                       # warm-up (code objects load lazily)
+  t0 = time.perf_counter()
+  eng.legacy_replay(t)
+  gen_s = time.perf_counter() - t0
+  eng.alloc_trace(t, 1)
+  eng.run(t)
+  ms, launches = eng.last_run_ms()
+  eng.close()
+  return {'workload': 'diag10 replay (reference-identical)', 'chains': n,
+          'steps': t, 'stream_gen_ms': gen_s * 1e3,
+          'stream_draws_per_s': n * t * 11 / gen_s,
+          'replay_kernel_ms': ms,
+          'chain_steps_per_s_kernel': n * t / (ms / 1e3),
+          'chain_steps_per_s_with_streams': n * t / (ms / 1e3 + gen_s),
+          'config': 'cfg2 shape, REPLAY mode fed by pbh_legacy_replay'}
+
+
 def main():
   import argparse
   ap = argparse.ArgumentParser()
-  ap.add_argument('--only', default='cfg1,cfg3,cfg5,lik',
-                  help='comma-separated subset of cfg1,cfg3,cfg5,lik')
+  ap.add_argument('--only', default='cfg1,cfg3,cfg5,lik,legacy',
+                  help='comma-separated subset of cfg1,cfg3,cfg5,lik,legacy')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--cpu-budget', type=float, default=4.0,
                   help='seconds of oracle work per cpu_baseline')
@@ -162,6 +191,8 @@ def main():
     lines.append(dict(o, config='cfg3'))
   if 'lik' in only:
     lines.append(bench_bool_perm_freq(cpu, args.cpu_budget))
+  if 'legacy' in only:
+    lines.append(bench_legacy_replay())
   if 'cfg5' not in only:
     for line in lines:
       print(json.dumps(line), flush=True)
