@@ -191,7 +191,7 @@ def main():
                                 else measured_traffic(n, spl, args.rng,
                                                       not args.no_trace),
                      'bytes_per_chain_step': bpcs,
-                     'kernel': 'mh_pair_kernel<10, PHILOX>' if not os.environ.get('PBH_NO_PAIR') else 'mh_kernel<10, PHILOX, DIAG, GAUSS>',
+                     'kernel': ('mh_pair_kernel<10, {}>' if not os.environ.get('PBH_NO_PAIR') else 'mh_kernel<10, {}, DIAG, GAUSS>').format(args.rng.upper()),
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),

@@ -1076,7 +1076,8 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
     double e = 0.;
 #pragma unroll
     for (int kk = 0; kk < KL; ++kk) e += fast_exp(v[kk] - M);
-    const double lpp = M + log(part_sum<L>(any ? e : 0.));
+    // the sum is in [1, K]: the production log (within 2 ulp) serves
+    const double lpp = M + fast_log(part_sum<L>(any ? e : 0.));
     // ---- acceptance (identical in every lane of the group) ----
     bool acc;
     if (!a.has_pred && s == 0) {

@@ -160,7 +160,7 @@ def main():
   ap.add_argument('--cpu-budget', type=float, default=4.0,
                   help='seconds of oracle work per cpu_baseline')
   ap.add_argument('--no-trace', action='store_true',
-                  help='cfg3 without the trace (arithmetic-only probe)')
+                  help='cfg3 / cfg5 without the trace (arithmetic-only probe)')
   args = ap.parse_args()
   only = args.only.split(',')
   cpu = not args.no_cpu_baseline
@@ -197,7 +197,13 @@ def main():
     for line in lines:
       print(json.dumps(line), flush=True)
     return
-  eng, o = run('gmm2', 32768, 2000)
+  eng, o = run('gmm2', 32768, 2000, trace=not args.no_trace)
+  if args.no_trace:
+    eng.close()
+    lines.append(dict(o, config='cfg5 per-GPU share, no trace'))
+    for line in lines:
+      print(json.dumps(line), flush=True)
+    return
   t0 = time.perf_counter()
   tr = eng.trace()
   eng.close()
