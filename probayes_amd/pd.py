@@ -135,6 +135,25 @@ class PD(dict):
             keys, set(self.keys()) - keys)
     return PD(self.name, dict(self), prob=self.prob, pscale=self.pscale)
 
+  def conditionalise(self, keys):
+    """pd.py:214-295.  On an MH / Gibbs summary every variable shares the
+    sample axis (dims {key: 0}); the reference then fails inside its own
+    arithmetic: conditionalising all keys sums over ``axis=None * ...`` and
+    raises TypeError, a strict subset moves axis 0 to axis 1 of a 1-D prob and
+    raises numpy's AxisError (recorded from the reference in
+    tests/golden/pd_ops.npz, ``cond_errors``).  The summary raises the same
+    exception types, so ``SP(samples, conditionalise=True)`` (sp.py:132-149,
+    196-197) fails as it does in the reference."""
+    keys = {keys} if isinstance(keys, str) else set(keys)
+    for key in keys:
+      assert key in self, 'Key {} not marginal in distribution {}'.format(
+          key, self.name)
+    if keys == set(self.keys()):
+      raise TypeError("unsupported operand type(s) for *: 'NoneType' and "
+                      "'int' (pd.py:284: summary prob has no axis to "
+                      "normalise over)")
+    raise np.exceptions.AxisError(1, 1, 'destination')
+
   def __repr__(self):
     keys = ','.join(self.keys())
     shape = None if self.prob is None else np.shape(self.prob)

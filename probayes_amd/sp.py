@@ -319,13 +319,23 @@ class SP:
     return steps
 
   def __call__(self, samples, **kwds):
-    """Summary of a walk (sp.py:131-198) as trace-backed PDs."""
+    """Summary of a walk (sp.py:131-198) as trace-backed PDs.  With
+    ``conditionalise=True`` the o, p and v summaries are conditionalised on
+    the leaf keys (sp.py:196-197), which the reference cannot do for a
+    summary (see PD.conditionalise)."""
+    conditionalise = kwds.pop('conditionalise', None)
     samples = list(samples)
     if not samples or not isinstance(samples[0], Step):
       raise TypeError('SP() summarises samples from SP.sampler()')
     sm = samples[0].sampler
     idx = np.array([s.i for s in samples])
-    return sm.summary(idx)
+    summary = sm.summary(idx)
+    if conditionalise:
+      for key in ('o', 'p', 'v'):
+        pd = getattr(summary, key)
+        if pd is not None:
+          summary = summary._replace(**{key: pd.conditionalise(list(pd.keys()))})
+    return summary
 
 
 OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',

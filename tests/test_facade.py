@@ -161,3 +161,18 @@ def test_covariance_tran_routes_like_the_reference():
   np.testing.assert_array_equal(spec['proposal']['tfun'], np.linalg.cholesky(cov))
   assert spec['proposal']['kind'] == 'uniform'
   assert spec['tran'] == {'kind': 'const', 'value': 1.0, 'sym': False}
+
+
+@pytest.mark.gpu
+def test_summary_conditionalise_fails_as_reference():
+  """SP(samples, conditionalise=True) (sp.py:132-149, 196-197) raises
+  TypeError on an MH summary in the reference (tests/golden/pd_ops.npz
+  meta cond_errors); the facade raises the same."""
+  builder, params, n, t, seed0 = WORKLOADS['diag10']
+  process, init, extra, kwds, keys, g = _build('diag10')
+  np.random.seed(int(g['seeds'][0]))
+  args = (init,) if extra is None else (init, extra)
+  samples = process.walk(process.sampler(*args, stop=8, **kwds))
+  assert process(samples).v is not None
+  with pytest.raises(TypeError):
+    process(samples, conditionalise=True)

@@ -76,3 +76,18 @@ def test_batched_summary_ops_are_per_chain():
   qb = sb.quantile([0.25, 0.75])
   q1 = s1.quantile([0.25, 0.75])
   assert qb[0][1][keys[0]] == q1[1][keys[0]]
+
+
+@pytest.mark.parametrize('case', [0, 1])
+def test_conditionalise_raises_as_reference(case):
+  """pd.py:214-295 on a summary raises; the exception types were recorded
+  from the reference (meta cond_errors: all keys, then the first key)."""
+  g, meta = _cases()
+  name, keys = meta['cases'][case]['name'], meta['cases'][case]['keys']
+  v = _pd(g, name, keys)
+  for ks, err in zip([keys, keys[:1]], meta['cases'][case]['cond_errors']):
+    with pytest.raises(Exception) as info:
+      v.conditionalise(ks)
+    assert type(info.value).__name__ == err
+  with pytest.raises(AssertionError):
+    v.conditionalise('not_a_key')

@@ -3,7 +3,8 @@ REFERENCE probayes in this container only (recipe: tools/gen_golden.py) and
 records, for MH summaries of a 1-variable and a 2-variable model, the summary
 values/probabilities together with the reference's own
 PD.expectation (pd.py:373-405), PD.sorted (pd.py:463-493) and
-PD.quantile (pd.py:408-460) outputs.  Output: tests/golden/pd_ops.npz.
+PD.quantile (pd.py:408-460) outputs, and the exception types
+PD.conditionalise (pd.py:214-295) raises on such summaries.  Output: tests/golden/pd_ops.npz.
 Nothing in tests/, bench.py or __graft_entry__ imports this script.
 """
 import json
@@ -75,6 +76,16 @@ def main():
           [float(next(iter(z))) if isinstance(z, set) else float(z) for z in qv])
       out['{}_quant_isset_{}'.format(name, k)] = np.array(
           [isinstance(z, set) for z in qv])
+    # conditionalise (pd.py:214-295) on a summary: record what the reference
+    # raises for all keys and for a strict subset
+    errs = []
+    for ks in [keys] + ([keys[:1]] if len(keys) > 1 else []):
+      try:
+        v.conditionalise(ks)
+        errs.append('')
+      except Exception as e:  # pylint: disable=broad-except
+        errs.append(type(e).__name__)
+    meta['cases'][-1]['cond_errors'] = errs
     uq = v.quantile(0.5)
     out['{}_unsorted_quant_isset'.format(name)] = np.array(
         [isinstance(uq[k], set) for k in keys])
