@@ -226,6 +226,32 @@ int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
                        const uint8_t *bool2d, int64_t *counts, int32_t reps,
                        double *kernel_ms);
 
+/* ---- user-conditional Gibbs: conjugate linear regression ---------------- */
+/* Replaces the per-chain loop of SP.next -> RF.eval_tfun (rf.py:413-462)
+ * over the user conditional cond_reg of examples/mcmc/gibbs_linreg.py:34-62
+ * (paras = beta_0 & beta_1 & y_sigma, tsteps = 1, gibbs scores), with
+ * v.prob = sum_j norm.logpdf(y_j, b0 + b1 x_j, y_sigma) + the joint uniform
+ * root priors (rf.py:541-562, rv_utils.py:30-38).
+ * hyper[6] = beta_0_mu, beta_0_sigma, beta_1_mu, beta_1_sigma,
+ *            y_sigma_alpha, y_sigma_beta (cond_reg's keyword defaults);
+ * vsets[6] = (lo, hi) of beta_0, beta_1, y_sigma.  Step k of the chain
+ * (absolute k = step0 + t) updates parameter k mod 3 (the RF's __cond_mod).
+ * init/final_x [3][n_chains]; rand [n_steps][n_chains] (REPLAY: the standard
+ * gauss, or standard_gamma(alpha + n_obs/2) on y_sigma steps, in NumPy's
+ * legacy order); trace_x [n_steps][3][n_chains], trace_lp [n_steps][n_chains]
+ * (either may be NULL).  rng_mode REPLAY / PHILOX_F64 use the reference's
+ * arithmetic; PHILOX uses sufficient statistics.  Host buffers; the chain
+ * runs `reps` >= 1 times from init on device-resident inputs after one
+ * untimed warm-up, *kernel_ms (may be NULL) = the average kernel time.     */
+int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
+                     const double *y_obs, const double *hyper,
+                     const double *vsets, int64_t n_chains,
+                     int64_t chain_offset, int64_t n_steps, int64_t step0,
+                     const double *init, int32_t rng_mode, uint64_t seed,
+                     const double *rand, double *trace_x, double *trace_lp,
+                     double *final_x, double *final_lp, int32_t reps,
+                     double *kernel_ms);
+
 /* ---- diagnostics -------------------------------------------------------- */
 /* Evaluates the production-mode acceptance filter and the exact ratio form
  * (sp_utils.py:40-64) on device for n triples (lp, lp', t = u01(t0, t1)).

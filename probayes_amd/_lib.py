@@ -110,6 +110,10 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_int64),
                                           ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_double)]),
+    'pbh_linreg_gibbs': (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_int64, _dp, _dp, _dp, _dp, ctypes.c_int64,
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _dp, ctypes.c_int32,
+        ctypes.c_uint64, _dp, _dp, _dp, _dp, _dp, ctypes.c_int32, _dp]),
 }
 
 

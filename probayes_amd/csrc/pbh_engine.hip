@@ -1131,4 +1131,133 @@ int pbh_check_normals(int device, int64_t n, const uint32_t *words,
   return PBH_OK;
 }
 
+
+// numpy's pairwise sum of a contiguous float64 array (the 8-accumulator
+// leaf of <= 128 terms, split at n/2 rounded down to a multiple of 8).
+static double np_pairwise_host(const double *a, int64_t n) {
+  if (n < 8) {
+    double r = 0.;
+    for (int64_t i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise_host(a, n2) + np_pairwise_host(a + n2, n - n2);
+}
+
+int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
+                     const double *y_obs, const double *hyper,
+                     const double *vsets, int64_t n_chains,
+                     int64_t chain_offset, int64_t n_steps, int64_t step0,
+                     const double *init, int32_t rng_mode, uint64_t seed,
+                     const double *rand, double *trace_x, double *trace_lp,
+                     double *final_x, double *final_lp, int32_t reps,
+                     double *kernel_ms) {
+  if (check_ptr(x_obs, "x_obs") || check_ptr(y_obs, "y_obs") ||
+      check_ptr(hyper, "hyper") || check_ptr(vsets, "vsets") ||
+      check_ptr(init, "init"))
+    return PBH_ERR_ARG;
+  if (n_obs < 1 || n_obs > pbh::linreg_max_obs())
+    return fail(PBH_ERR_ARG, "n_obs must be in 1..%lld, got %lld",
+                (long long)pbh::linreg_max_obs(), (long long)n_obs);
+  if (n_chains < 1 || n_steps < 0 || step0 < 0 || chain_offset < 0)
+    return fail(PBH_ERR_ARG, "n_chains must be >= 1 and n_steps, step0, "
+                "chain_offset >= 0");
+  if (rng_mode != PBH_RNG_REPLAY && rng_mode != PBH_RNG_PHILOX &&
+      rng_mode != PBH_RNG_PHILOX_F64)
+    return fail(PBH_ERR_UNSUPPORTED, "pbh_linreg_gibbs: rng_mode %d", rng_mode);
+  if (rng_mode == PBH_RNG_REPLAY && n_steps > 0 && !rand)
+    return fail(PBH_ERR_ARG, "REPLAY needs rand [n_steps][n_chains]");
+  if (reps < 1) return fail(PBH_ERR_ARG, "reps must be >= 1");
+  if (hyper[1] == 0. || hyper[3] == 0.)
+    return fail(PBH_ERR_ARG, "prior sigmas must be non-zero");
+  const double alpha_post = hyper[4] + 0.5 * (double)n_obs;
+  if (!(alpha_post >= 1.))
+    return fail(PBH_ERR_ARG, "y_sigma_alpha + n_obs/2 must be >= 1");
+  pbh::LinregArgs h{};
+  std::vector<double> sq(n_obs);
+  double sx = 0., sy = 0., sxy = 0., syy = 0.;
+  for (int64_t j = 0; j < n_obs; ++j) {
+    sq[j] = x_obs[j] * x_obs[j];
+    sx += x_obs[j]; sy += y_obs[j];
+    sxy += x_obs[j] * y_obs[j]; syy += y_obs[j] * y_obs[j];
+  }
+  h.hyper[0] = 1. / (hyper[1] * hyper[1]); h.hyper[1] = hyper[0];
+  h.hyper[2] = 1. / (hyper[3] * hyper[3]); h.hyper[3] = hyper[2];
+  h.hyper[4] = alpha_post; h.hyper[5] = hyper[5];
+  h.hyper[6] = np_pairwise_host(sq.data(), n_obs);
+  for (int k = 0; k < 3; ++k) h.hyper[7 + k] = -std::log(vsets[2 * k + 1] - vsets[2 * k]);
+  h.hyper[10] = std::log(std::sqrt(2. * M_PI));
+  h.stats[0] = sx; h.stats[1] = sy; h.stats[2] = sxy; h.stats[3] = syy;
+  h.n_obs = n_obs; h.n = n_chains; h.chain_offset = chain_offset;
+  h.n_steps = n_steps; h.step0 = step0; h.seed = seed; h.mode = rng_mode;
+  if (kernel_ms) *kernel_ms = 0.;
+  HIP_TRY(hipSetDevice(device));
+  const int64_t T = n_steps, N = n_chains;
+  double *dxo = nullptr, *dyo = nullptr, *dinit = nullptr, *dstate = nullptr,
+         *dlp = nullptr, *drand = nullptr, *dtx = nullptr, *dtp = nullptr;
+  int rc = dalloc(dxo, n_obs);
+  if (!rc) rc = dalloc(dyo, n_obs);
+  if (!rc) rc = dalloc(dinit, 3 * N);
+  if (!rc) rc = dalloc(dstate, 3 * N);
+  if (!rc) rc = dalloc(dlp, N);
+  if (!rc && rng_mode == PBH_RNG_REPLAY && T > 0) rc = dalloc(drand, T * N);
+  if (!rc && T > 0) rc = dalloc(dtx, T * 3 * N);
+  if (!rc && T > 0) rc = dalloc(dtp, T * N);
+  hipError_t err = hipSuccess;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double total = 0.;
+  if (!rc) {
+    err = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (err == hipSuccess) err = hipEventCreate(&e0);
+    if (err == hipSuccess) err = hipEventCreate(&e1);
+    if (err == hipSuccess) err = hipMemcpy(dxo, x_obs, n_obs * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(dyo, y_obs, n_obs * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(dinit, init, 3 * N * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess && drand)
+      err = hipMemcpy(drand, rand, T * N * 8, hipMemcpyHostToDevice);
+    h.x_obs = dxo; h.y_obs = dyo; h.state = dstate; h.lp_state = dlp;
+    h.rand = drand; h.tx = dtx; h.tp = dtp;
+    for (int r = 0; r <= reps && err == hipSuccess && T > 0; ++r) {
+      err = hipMemcpyAsync(dstate, dinit, 3 * N * 8, hipMemcpyDeviceToDevice, st);
+      if (err == hipSuccess) err = hipEventRecord(e0, st);
+      if (err == hipSuccess) err = pbh::launch_linreg_gibbs(h, st);
+      if (err == hipSuccess) err = hipEventRecord(e1, st);
+      if (err == hipSuccess) err = hipEventSynchronize(e1);
+      float ms = 0.f;
+      if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+      if (r > 0) total += ms;
+    }
+    if (err == hipSuccess && trace_x && T > 0)
+      err = hipMemcpy(trace_x, dtx, T * 3 * N * 8, hipMemcpyDeviceToHost);
+    if (err == hipSuccess && trace_lp && T > 0)
+      err = hipMemcpy(trace_lp, dtp, T * N * 8, hipMemcpyDeviceToHost);
+    if (err == hipSuccess && final_x)
+      err = hipMemcpy(final_x, T > 0 ? dstate : dinit, 3 * N * 8, hipMemcpyDeviceToHost);
+    if (err == hipSuccess && final_lp && T > 0)
+      err = hipMemcpy(final_lp, dlp, N * 8, hipMemcpyDeviceToHost);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  dfree(dxo); dfree(dyo); dfree(dinit); dfree(dstate); dfree(dlp);
+  dfree(drand); dfree(dtx); dfree(dtp);
+  if (rc) return rc;
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_linreg_gibbs: %s", hipGetErrorString(err));
+  if (kernel_ms) *kernel_ms = total / reps;
+  return PBH_OK;
+}
+
 }  // extern "C"

@@ -122,4 +122,21 @@ hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
                                const uint32_t *t0, const uint32_t *t1,
                                int32_t lin, double log_npi, uint8_t *out);
 
+// user-conditional Gibbs of the gibbs_linreg model (pbh_linreg.hip).
+// hyper: p0, m0, p1, m1, alpha_post, beta, sxx, prior[3], logC;
+// stats: Sx, Sy, Sxy, Syy (PHILOX's fast form).
+struct LinregArgs {
+  const double *x_obs, *y_obs;
+  int64_t n_obs;
+  double hyper[11], stats[4];
+  double *state, *lp_state;
+  const double *rand;
+  double *tx, *tp;
+  int64_t n, chain_offset, n_steps, step0;
+  uint64_t seed;
+  int32_t mode;
+};
+int64_t linreg_max_obs();
+hipError_t launch_linreg_gibbs(const LinregArgs &a, hipStream_t s);
+
 }  // namespace pbh

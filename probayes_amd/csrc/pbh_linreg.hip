@@ -1,0 +1,212 @@
+// pbh_linreg.hip -- user-conditional (tfun) Gibbs for the conjugate linear
+// regression of examples/mcmc/gibbs_linreg.py on gfx950.
+//
+// Reference path: SP.next -> RF.eval_tfun (rf.py:413-462) calls the user
+// conditional cond_reg (gibbs_linreg.py:34-62) for ONE parameter per step,
+// cycling beta_0, beta_1, y_sigma through the RF's __cond_mod (rf.py:446-452);
+// gibbs scores accept every step (sp_utils.py:75-84); v.prob is the iid sum
+// of norm.logpdf(y, b0 + b1 x, y_sigma) over the observations (rf.py:541-562)
+// plus the joint uniform root priors (rv_utils.py:30-38).
+//
+// One chain per lane; the observations (x, y) are staged once per workgroup in
+// LDS and read with wave-uniform addresses (LDS broadcast, no bank conflicts).
+// Two arithmetic forms:
+//   EXACT (REPLAY, PHILOX_F64): the reference's operations -- numpy's pairwise
+//     sums over the observations, true IEEE divisions, scipy's logpdf -- so a
+//     REPLAY run reproduces the reference chain from its standard draws;
+//   FAST (PHILOX): the sums come from the sufficient statistics Sx, Sy, Sxx,
+//     Sxy, Syy (O(1) per step instead of O(n)); same conditional law.
+// Draws: REPLAY reads the standard gauss / standard_gamma(a + n/2) of each step
+// from rand[T][N]; PHILOX modes draw fp64 Box-Muller normals and
+// Marsaglia-Tsang gammas from Philox-4x32-10 keyed by (seed, global chain),
+// counter (absolute step, attempt).
+// Trace: x [T][3][N] (chain fastest), lp [T][N]; every step is accepted.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "../../include/pbhip.h"
+#include "pbh_device.h"
+#include "pbh_kernels.h"
+
+namespace pbh {
+namespace {
+
+constexpr int kBlock = 256;
+
+// scipy norm.logpdf(x, loc, scale) = _norm_logpdf((x - loc) / scale) -
+// log(scale), _norm_logpdf(y) = -y**2 / 2.0 - _norm_pdf_logC.
+__device__ __forceinline__ double lr_norm_logpdf(double x, double loc,
+                                                 double scale, double logscale,
+                                                 double logC) {
+  const double y = (x - loc) / scale;
+  return ((-(y * y)) / 2.0 - logC) - logscale;
+}
+
+struct LinregK {
+  const double *x_obs, *y_obs;
+  int64_t n_obs;
+  // hyper: p0, m0, p1, m1 (prior precisions and means), alpha_post, beta0,
+  // sxx = np.sum(x**2) (host), prior[3], logC, and the sufficient statistics
+  // Sx, Sy, Sxy, Syy (FAST only)
+  double p0, m0, p1, m1, alpha, beta, sxx, pri0, pri1, pri2, logC;
+  double sx, sy, sxy, syy;
+  double *state;          // [3][n] beta_0, beta_1, y_sigma (in/out)
+  double *lp_state;       // [n] (out)
+  const double *rand;     // REPLAY [T][n]
+  double *tx, *tp;        // trace [T][3][n], [T][n]
+  int64_t n, chain_offset, n_steps, step0;
+  uint64_t seed;
+  int32_t mode;           // PBH_RNG_REPLAY / PHILOX / PHILOX_F64
+};
+
+__device__ __forceinline__ u32x4 draw_block(const LinregK &a, int64_t gc,
+                                            int64_t step, uint32_t attempt) {
+  return philox4x32_10(u32x4{(uint32_t)step, (uint32_t)(step >> 32), attempt,
+                             0x4c524547u /* "LREG" */},
+                       (uint32_t)(a.seed ^ (uint64_t)gc * 0x9E3779B97F4A7C15ull),
+                       (uint32_t)((a.seed >> 32) ^ (uint64_t)(gc >> 32)) + (uint32_t)gc);
+}
+
+// Marsaglia & Tsang (2000) for shape a >= 1: d = a - 1/3, c = 1/sqrt(9d);
+// z ~ N(0,1), v = (1 + c z)^3; accept d v when v > 0 and
+// log u < z^2/2 + d - d v + d log v.  Acceptance > 0.98 at the shapes here;
+// every attempt uses a fresh counter, so the loop ends with probability 1
+// (capped at 64 attempts, beyond which the last proposal is returned).
+__device__ __forceinline__ double mt_gamma(const LinregK &a, int64_t gc,
+                                           int64_t step) {
+  const double d = a.alpha - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  double out = d;
+  for (uint32_t att = 1; att <= 64; ++att) {
+    const u32x4 w = draw_block(a, gc, step, att);
+    double z, z1;
+    box_muller(u32x4{w.x, w.y, w.z, w.w}, z, z1);
+    const double t = 1.0 + c * z;
+    if (t <= 0.0) continue;
+    const double v = t * t * t;
+    out = d * v;
+    // the second deviate's block supplies the uniform
+    const u32x4 w2 = draw_block(a, gc, step, att + 0x10000u);
+    const double u = 1.0 - u01(w2.x, w2.y);  // (0, 1]
+    if (log(u) < 0.5 * z * z + d - d * v + d * log(v)) break;
+  }
+  return out;
+}
+
+template <bool EXACT>
+__global__ void __launch_bounds__(kBlock)
+linreg_gibbs_kernel(LinregK a) {
+  extern __shared__ double lds[];
+  double *xs = lds, *ys_obs = lds + a.n_obs;
+  if (EXACT) {
+    for (int64_t j = threadIdx.x; j < a.n_obs; j += blockDim.x) {
+      xs[j] = a.x_obs[j];
+      ys_obs[j] = a.y_obs[j];
+    }
+    __syncthreads();
+  }
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  const int64_t gc = a.chain_offset + c;
+  const int64_t n = a.n;
+  double b0 = a.state[c], b1 = a.state[n + c], sg = a.state[2 * n + c];
+  const double nd = (double)a.n_obs;
+  double lp = 0.;
+  for (int64_t t = 0; t < a.n_steps; ++t) {
+    const int64_t step = a.step0 + t;
+    const int key = (int)(step % 3);
+    double z;
+    if (a.mode == PBH_RNG_REPLAY) {
+      z = a.rand[t * n + c];
+    } else if (key == 2) {
+      z = mt_gamma(a, gc, step);
+    } else {
+      double z1;
+      box_muller(draw_block(a, gc, step, 0), z, z1);
+    }
+    if (key == 2) {
+      // cond_beta = b + 0.5 * sum((y - b0 - b1 x)**2); 1/sqrt(gamma(a, 1/cb))
+      double ss;
+      if (EXACT) {
+        ss = np_pairwise([&](int64_t j) {
+          const double r = (ys_obs[j] - b0) - b1 * xs[j];
+          return r * r;
+        }, a.n_obs);
+      } else {
+        ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx - 2.0 * b0 * a.sy -
+             2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
+      }
+      const double cb = a.beta + 0.5 * ss;
+      sg = 1.0 / sqrt((1.0 / cb) * z);
+    } else {
+      const double yp = 1.0 / (sg * sg);
+      if (key == 0) {
+        const double v = 1.0 / (a.p0 + nd * yp);
+        const double s = EXACT ? np_pairwise([&](int64_t j) {
+          return ys_obs[j] - b1 * xs[j]; }, a.n_obs) : a.sy - b1 * a.sx;
+        const double m = (a.p0 * a.m0 + yp * s) * v;
+        b0 = m + sqrt(v) * z;
+      } else {
+        const double v = 1.0 / (a.p1 + yp * a.sxx);
+        const double s = EXACT ? np_pairwise([&](int64_t j) {
+          return xs[j] * (ys_obs[j] - b0); }, a.n_obs) : a.sxy - b0 * a.sx;
+        const double m = (a.p1 * a.m1 + yp * s) * v;
+        b1 = m + sqrt(v) * z;
+      }
+    }
+    // v.prob: sum_j norm.logpdf(y_j, b0 + b1 x_j, sg) + the root priors
+    const double lsg = log(sg);
+    if (EXACT) {
+      lp = np_pairwise([&](int64_t j) {
+        return lr_norm_logpdf(ys_obs[j], b0 + b1 * xs[j], sg, lsg, a.logC);
+      }, a.n_obs);
+    } else {
+      const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx -
+                        2.0 * b0 * a.sy - 2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
+      lp = -0.5 * ss / (sg * sg) - nd * (a.logC + lsg);
+    }
+    lp = ((lp + a.pri0) + a.pri1) + a.pri2;
+    double *tx = a.tx + t * 3 * n;
+    __builtin_nontemporal_store(b0, tx + c);
+    __builtin_nontemporal_store(b1, tx + n + c);
+    __builtin_nontemporal_store(sg, tx + 2 * n + c);
+    __builtin_nontemporal_store(lp, a.tp + t * n + c);
+  }
+  a.state[c] = b0;
+  a.state[n + c] = b1;
+  a.state[2 * n + c] = sg;
+  a.lp_state[c] = lp;
+}
+
+}  // namespace
+
+int64_t linreg_max_obs() { return 8192; }  // 2 x 8192 x 8 B = 128 KB of LDS
+
+hipError_t launch_linreg_gibbs(const LinregArgs &h, hipStream_t s) {
+  LinregK a;
+  a.x_obs = h.x_obs; a.y_obs = h.y_obs; a.n_obs = h.n_obs;
+  a.p0 = h.hyper[0]; a.m0 = h.hyper[1]; a.p1 = h.hyper[2]; a.m1 = h.hyper[3];
+  a.alpha = h.hyper[4]; a.beta = h.hyper[5]; a.sxx = h.hyper[6];
+  a.pri0 = h.hyper[7]; a.pri1 = h.hyper[8]; a.pri2 = h.hyper[9];
+  a.logC = h.hyper[10];
+  a.sx = h.stats[0]; a.sy = h.stats[1]; a.sxy = h.stats[2]; a.syy = h.stats[3];
+  a.state = h.state; a.lp_state = h.lp_state; a.rand = h.rand;
+  a.tx = h.tx; a.tp = h.tp;
+  a.n = h.n; a.chain_offset = h.chain_offset; a.n_steps = h.n_steps;
+  a.step0 = h.step0; a.seed = h.seed; a.mode = h.mode;
+  const dim3 grid((unsigned)((h.n + kBlock - 1) / kBlock)), block(kBlock);
+  if (h.mode == PBH_RNG_PHILOX) {
+    hipLaunchKernelGGL(linreg_gibbs_kernel<false>, grid, block, 0, s, a);
+  } else {
+    const size_t lds = (size_t)(2 * h.n_obs) * sizeof(double);
+    if (lds > 65536) {
+      const hipError_t e = hipFuncSetAttribute(
+          (const void *)linreg_gibbs_kernel<true>,
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(linreg_gibbs_kernel<true>, grid, block, lds, s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pbh

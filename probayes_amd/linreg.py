@@ -1,0 +1,108 @@
+"""User-conditional Gibbs for the conjugate linear regression of
+examples/mcmc/gibbs_linreg.py, on the GPU.
+
+The reference runs `RF.set_tfun(cond_reg, tsteps=1, x=x_obs, y=y_obs)` on
+paras = beta_0 & beta_1 & y_sigma with `SP.set_scores('gibbs')`: each SP.next
+calls cond_reg for ONE parameter (rf.py:413-462, cycling through __cond_mod),
+accepts it (sp_utils.py:75-84) and evaluates v.prob = the iid sum of
+norm.logpdf(y, b0 + b1 x, y_sigma) plus the joint uniform root priors
+(rf.py:541-562, rv_utils.py:30-38).
+
+`LinRegConditional` is a plain callable with cond_reg's signature and
+NumPy-global draws, so the SAME object runs in the reference as the user tfun;
+the façade (`SP.lower`) recognises it and lowers the process to
+`pbh_linreg_gibbs` (probayes_amd/csrc/pbh_linreg.hip).  Other user tfuns raise
+NotLowerable.  `run` is the batched entry: all chains in one kernel launch.
+"""
+import ctypes
+
+import numpy as np
+
+from probayes_amd import _lib
+
+_dp = ctypes.POINTER(ctypes.c_double)
+KEYS = ('beta_0', 'beta_1', 'y_sigma')
+
+
+def _ptr(a):
+  return None if a is None else a.ctypes.data_as(_dp)
+
+
+class LinRegConditional:
+  """cond_reg of gibbs_linreg.py:34-62 as a descriptor: draws the conditional
+  of `unknown` given the others with np.random.gamma / np.random.normal, in
+  the reference's arithmetic."""
+
+  def __init__(self, n_obs, beta_0_mu=0., beta_0_sigma=1., beta_1_mu=0.,
+               beta_1_sigma=1., y_sigma_alpha=1., y_sigma_beta=1.):
+    self.n_obs = int(n_obs)
+    self.hyper = (float(beta_0_mu), float(beta_0_sigma), float(beta_1_mu),
+                  float(beta_1_sigma), float(y_sigma_alpha),
+                  float(y_sigma_beta))
+
+  def __call__(self, x, y, beta_0, beta_1, y_sigma, unknown):
+    m0, s0, m1, s1, a, b = self.hyper
+    n = self.n_obs
+    if unknown == 'y_sigma':
+      cond_alpha = a + 0.5 * n
+      cond_beta = b + 0.5 * np.sum((y - beta_0 - beta_1 * x) ** 2)
+      return 1 / np.sqrt(np.random.gamma(cond_alpha, 1 / cond_beta))
+    y_prec = 1 / (y_sigma ** 2)
+    if unknown == 'beta_0':
+      p0 = 1 / (s0 ** 2)
+      cond_var = 1 / (p0 + n * y_prec)
+      cond_mu = (p0 * m0 + y_prec * np.sum(y - beta_1 * x)) * cond_var
+      return np.random.normal(cond_mu, np.sqrt(cond_var))
+    if unknown == 'beta_1':
+      p1 = 1 / (s1 ** 2)
+      cond_var = 1 / (p1 + y_prec * np.sum(x ** 2))
+      cond_mu = (p1 * m1 + y_prec * np.sum(x * (y - beta_0))) * cond_var
+      return np.random.normal(cond_mu, np.sqrt(cond_var))
+    raise ValueError("Unknown unknown: {}".format(unknown))
+
+
+def run(x_obs, y_obs, init, n_steps, hyper=(0., 1., 0., 1., 1., 1.),
+        vsets=((-6., 6.), (-6., 6.), (0.001, 10.)), rng='philox', seed=0,
+        rand=None, step0=0, chain_offset=0, device=0, reps=1, trace=True):
+  """Runs N chains for n_steps on the GPU.  init [N, 3] (beta_0, beta_1,
+  y_sigma).  rng 'replay' reads rand [n_steps, N] (standard draws in NumPy's
+  legacy order); 'philox' (fast sufficient-statistics form) and 'philox_f64'
+  (reference arithmetic) draw on the device.  Returns a dict with v_x
+  [N, T, 3], v_p [N, T] (when trace), final_x [N, 3], final_p [N] and the
+  average kernel ms."""
+  x_obs = np.ascontiguousarray(x_obs, np.float64)
+  y_obs = np.ascontiguousarray(y_obs, np.float64)
+  if x_obs.shape != y_obs.shape or x_obs.ndim != 1:
+    raise ValueError('x_obs and y_obs must be 1-D of the same length')
+  init = np.asarray(init, np.float64)
+  if init.ndim != 2 or init.shape[1] != 3:
+    raise ValueError('init must be [N, 3]')
+  n = init.shape[0]
+  T = int(n_steps)
+  mode = _lib.RNG[rng]
+  if mode == _lib.RNG['xoshiro']:
+    raise ValueError('linreg Gibbs supports replay, philox and philox_f64')
+  if mode == _lib.RNG['replay']:
+    rand = np.ascontiguousarray(rand, np.float64)
+    if rand.shape != (T, n):
+      raise ValueError('rand must be [n_steps, N] = {}'.format((T, n)))
+  else:
+    rand = None
+  h = np.asarray(hyper, np.float64)
+  v = np.asarray(vsets, np.float64).reshape(6)
+  init_t = np.ascontiguousarray(init.T)
+  tx = np.empty((T, 3, n)) if trace and T else None
+  tp = np.empty((T, n)) if trace and T else None
+  fx = np.empty((3, n))
+  fp = np.full(n, np.nan)
+  ms = ctypes.c_double(0.)
+  _lib.call('pbh_linreg_gibbs', int(device), len(x_obs), _ptr(x_obs),
+            _ptr(y_obs), _ptr(h), _ptr(v), n, int(chain_offset), T,
+            int(step0), _ptr(init_t), mode, ctypes.c_uint64(int(seed)),
+            _ptr(rand), _ptr(tx), _ptr(tp), _ptr(fx), _ptr(fp), int(reps),
+            ctypes.byref(ms))
+  out = {'final_x': fx.T.copy(), 'final_p': fp, 'ms': ms.value}
+  if tx is not None:
+    out['v_x'] = np.transpose(tx, (2, 0, 1)).copy()
+    out['v_p'] = tp.T.copy()
+  return out

@@ -315,3 +315,70 @@ def _covrw5_params():
 
 WORKLOADS['covrw2'] = (covrw2, {'step': 0.5}, 16, 256, 12000)
 WORKLOADS['covrw5'] = (covrw5, _covrw5_params(), 16, 256, 13000)
+
+
+def _linreg_params():
+  rs = np.random.RandomState(321)
+  x_obs = rs.normal(0, 1, size=60)
+  y_obs = rs.normal(1.5 * x_obs - 1., 0.5)
+  return {'x_obs': x_obs, 'y_obs': y_obs,
+          'init': np.array([-0.9, 1.4, 0.6])}
+
+
+def linreg_cond(x_obs, y_obs):
+  """The conditional sampler of examples/mcmc/gibbs_linreg.py:34-62 (cond_reg)
+  with the example's default hyper-parameters, closed over the data size."""
+  rand_size = len(x_obs)
+
+  def cond_reg(x, y, beta_0, beta_1, y_sigma, unknown,
+               beta_0_mu=0, beta_0_sigma=1, beta_1_mu=0, beta_1_sigma=1.,
+               y_sigma_alpha=1., y_sigma_beta=1.):
+    if unknown == 'y_sigma':
+      cond_alpha = y_sigma_alpha + 0.5 * rand_size
+      cond_beta = y_sigma_beta + 0.5 * np.sum((y - beta_0 - beta_1 * x) ** 2)
+      return 1 / np.sqrt(np.random.gamma(cond_alpha, 1 / cond_beta))
+    y_prec = 1 / (y_sigma ** 2)
+    if unknown == 'beta_0':
+      beta_0_prec = 1 / (beta_0_sigma ** 2)
+      cond_var = 1 / (beta_0_prec + rand_size * y_prec)
+      cond_mu = (beta_0_prec * beta_0_mu + y_prec * np.sum(y - beta_1 * x)) \
+          * cond_var
+      return np.random.normal(cond_mu, np.sqrt(cond_var))
+    if unknown == 'beta_1':
+      beta_1_prec = 1 / (beta_1_sigma ** 2)
+      cond_var = 1 / (beta_1_prec + y_prec * np.sum(x ** 2))
+      cond_mu = (beta_1_prec * beta_1_mu + y_prec * np.sum(x * (y - beta_0))) \
+          * cond_var
+      return np.random.normal(cond_mu, np.sqrt(cond_var))
+    raise ValueError("Unknown unknown: {}".format(unknown))
+  return cond_reg
+
+
+def gibbs_linreg(pb, params):
+  """examples/mcmc/gibbs_linreg.py:26-80 (user-tfun Gibbs, rf.py:464-487),
+  data from a fixed RandomState instead of the global stream."""
+  x_obs, y_obs = params['x_obs'], params['y_obs']
+  x = pb.RV('x', vtype=float, vset=[-3, 3])
+  y = pb.RV('y', vtype=float, vset=[-np.inf, np.inf])
+  beta_0 = pb.RV('beta_0', vtype=float, vset=[-6., 6.])
+  beta_1 = pb.RV('beta_1', vtype=float, vset=[-6., 6.])
+  y_sigma = pb.RV('y_sigma', vtype=float, vset=[(0.001), 10.])
+
+  def norm_reg(x, y, beta_0, beta_1, y_sigma):
+    return scipy.stats.norm.logpdf(y, loc=beta_0 + beta_1 * x, scale=y_sigma)
+
+  stats = x & y
+  paras = beta_0 & beta_1 & y_sigma
+  paras.set_tfun(linreg_cond(x_obs, y_obs), tsteps=1, x=x_obs, y=y_obs)
+  process = pb.SP(stats, paras)
+  process.set_tfun(paras)
+  process.set_prob(norm_reg, pscale='log')
+  process.set_scores('gibbs')
+  init = dict(zip(['beta_0', 'beta_1', 'y_sigma'], params['init']))
+  return (process, init, {'x,y': [x_obs, y_obs]},
+          {'iid': True, 'joint': True}, ['beta_0', 'beta_1', 'y_sigma'])
+
+
+# user-tfun Gibbs: lowered by probayes_amd.linreg, not the generic spec
+# (oracle/linreg.py, tests/test_linreg.py)
+TFUN_WORKLOADS = {'gibbs_linreg': (gibbs_linreg, _linreg_params(), 8, 96, 14000)}

@@ -1,0 +1,138 @@
+"""User-conditional Gibbs (examples/mcmc/gibbs_linreg.py): the oracle against
+the reference's recorded chains, the descriptor conditional, the C-ABI's
+argument errors (CPU), and the HIP kernel against the oracle (GPU)."""
+import numpy as np
+import pytest
+
+from oracle.linreg import linreg_streams, run_linreg, HYPER, VSETS
+from probayes_amd import _lib, linreg
+
+GOLDEN = 'tests/golden/gibbs_linreg.npz'
+
+
+def _golden(root):
+  import os
+  g = np.load(os.path.join(root, GOLDEN))
+  n = len(g['seeds'])
+  return g, g['param_x_obs'], g['param_y_obs'], np.tile(g['param_init'], (n, 1))
+
+
+def test_oracle_matches_reference_bitwise(root):
+  """tools/gen_golden.py recorded the reference's SP chains (rf.py:413-462
+  calling cond_reg; fresh SP per chain, np.random.seed(seed))."""
+  g, x, y, init = _golden(root)
+  t = g['v_x'].shape[1]
+  o = run_linreg(x, y, init, linreg_streams(g['seeds'], t, len(x)))
+  assert np.array_equal(o['v_x'], g['v_x'])
+  assert np.array_equal(o['v_p'], g['v_p'])
+  assert np.all(g['u'] == 1)            # gibbs: every step accepted
+  assert np.array_equal(g['p_x'], g['v_x'])
+
+
+def test_descriptor_conditional_draws_like_cond_reg(root):
+  """LinRegConditional in the reference's calling convention (one unknown per
+  call, NumPy's global stream) gives the golden chain."""
+  g, x, y, init = _golden(root)
+  cond = linreg.LinRegConditional(len(x))
+  for c in range(2):
+    np.random.seed(int(g['seeds'][c]))
+    vals = dict(zip(linreg.KEYS, init[c]))
+    for t in range(g['v_x'].shape[1]):
+      key = linreg.KEYS[t % 3]
+      vals[key] = cond(x, y, unknown=key, **vals)
+      assert [vals[k] for k in linreg.KEYS] == list(g['v_x'][c, t])
+
+
+def test_abi_rejects_bad_arguments():
+  x = np.zeros(4)
+  init = np.ones((2, 3))
+  with pytest.raises(ValueError):
+    linreg.run(x, np.zeros(5), init, 3)
+  with pytest.raises(_lib.PbhError):    # n_obs above the LDS cap
+    linreg.run(np.zeros(10000), np.zeros(10000), init, 3)
+  with pytest.raises(ValueError):       # replay needs [T, N] draws
+    linreg.run(x, x, init, 3, rng='replay', rand=np.zeros((2, 2)))
+  with pytest.raises(_lib.PbhError):
+    linreg.run(x, x, init, 3, hyper=(0., 0., 0., 1., 1., 1.))
+
+
+def _data(n_obs, seed=5):
+  rs = np.random.RandomState(seed)
+  x = rs.normal(0, 1, size=n_obs)
+  return x, rs.normal(1.5 * x - 1., 0.5)
+
+
+@pytest.mark.gpu
+def test_replay_reproduces_reference_chains(root):
+  g, x, y, init = _golden(root)
+  t = g['v_x'].shape[1]
+  st = linreg_streams(g['seeds'], t, len(x))
+  out = linreg.run(x, y, init, t, rng='replay', rand=st)
+  rel = np.abs(out['v_x'] - g['v_x']) / np.maximum(np.abs(g['v_x']), 1.)
+  assert rel.max() <= 1e-12, rel.max()
+  assert np.max(np.abs(out['v_p'] - g['v_p']) / np.abs(g['v_p'])) <= 1e-12
+  assert np.array_equal(out['final_x'], out['v_x'][:, -1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('n_obs', [1, 7, 60, 129, 1000, 8192])
+def test_replay_matches_oracle_ragged(n_obs):
+  """Edge sizes of the pairwise sums (n < 8, leaf, split tree, LDS cap) and
+  a ragged chain count."""
+  x, y = _data(n_obs)
+  n, t = 77, 40
+  init = np.column_stack([np.full(n, -0.5), np.full(n, 1.0),
+                          np.linspace(0.3, 2., n)])
+  st = linreg_streams(np.arange(100, 100 + n), t, n_obs)
+  ref = run_linreg(x, y, init, st)
+  out = linreg.run(x, y, init, t, rng='replay', rand=st)
+  rel = np.abs(out['v_x'] - ref['v_x']) / np.maximum(np.abs(ref['v_x']), 1.)
+  assert rel.max() <= 1e-12, rel.max()
+  relp = np.abs(out['v_p'] - ref['v_p']) / np.maximum(np.abs(ref['v_p']), 1.)
+  assert relp.max() <= 1e-12, relp.max()
+
+
+@pytest.mark.gpu
+def test_fast_form_matches_reference_arithmetic_on_the_same_draws():
+  """PHILOX (sufficient statistics) and PHILOX_F64 (reference arithmetic)
+  read the same Philox draws: the chains agree to rounding."""
+  x, y = _data(60)
+  n, t = 4096, 300
+  init = np.tile([-0.9, 1.4, 0.6], (n, 1))
+  a = linreg.run(x, y, init, t, rng='philox', seed=11)
+  b = linreg.run(x, y, init, t, rng='philox_f64', seed=11)
+  assert np.max(np.abs(a['v_x'] - b['v_x'])) <= 1e-9
+  assert np.max(np.abs(a['v_p'] - b['v_p']) / np.abs(b['v_p'])) <= 1e-9
+
+
+@pytest.mark.gpu
+def test_sharding_and_launch_split_invariance():
+  x, y = _data(60)
+  n, t = 1000, 60
+  init = np.tile([-0.9, 1.4, 0.6], (n, 1))
+  full = linreg.run(x, y, init, t, rng='philox', seed=3)
+  lo = linreg.run(x, y, init[:400], t, rng='philox', seed=3)
+  hi = linreg.run(x, y, init[400:], t, rng='philox', seed=3, chain_offset=400)
+  assert np.array_equal(np.concatenate([lo['v_x'], hi['v_x']]), full['v_x'])
+  first = linreg.run(x, y, init, 25, rng='philox', seed=3)
+  second = linreg.run(x, y, first['final_x'], t - 25, rng='philox', seed=3,
+                      step0=25)
+  assert np.array_equal(second['v_x'], full['v_x'][:, 25:])
+
+
+@pytest.mark.gpu
+def test_posterior_matches_oracle_within_monte_carlo_error():
+  """Posterior means and sds of (beta_0, beta_1, y_sigma) from Philox chains
+  against the oracle's NumPy-stream chains (the reference's law)."""
+  x, y = _data(60, seed=9)
+  burn, t = 30, 150
+  n_gpu, n_cpu = 16384, 2048
+  init = np.tile([0., 0., 1.], (n_gpu, 1))
+  g = linreg.run(x, y, init, t, rng='philox', seed=21)['v_x'][:, burn:]
+  r = run_linreg(x, y, init[:n_cpu], linreg_streams(
+      np.arange(5000, 5000 + n_cpu), t, len(x)))['v_x'][:, burn:]
+  for k in range(3):
+    gm, rm = g[:, -1, k].mean(), r[:, -1, k].mean()
+    sd = r[:, -1, k].std()
+    assert abs(gm - rm) <= 5 * sd * np.sqrt(1 / n_gpu + 1 / n_cpu), (k, gm, rm)
+    assert abs(g[:, -1, k].std() / sd - 1) <= 0.1, k

@@ -48,7 +48,8 @@ def _pb():
   return pb
 
 
-from mcmc_examples import WORKLOADS  # noqa: E402  (builders shared with tests)
+from mcmc_examples import WORKLOADS, TFUN_WORKLOADS  # noqa: E402
+WORKLOADS = dict(WORKLOADS, **TFUN_WORKLOADS)  # builders shared with tests
 
 
 def _nan(v):
