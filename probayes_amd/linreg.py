@@ -106,3 +106,41 @@ def run(x_obs, y_obs, init, n_steps, hyper=(0., 1., 0., 1., 1., 1.),
     out['v_x'] = np.transpose(tx, (2, 0, 1)).copy()
     out['v_p'] = tp.T.copy()
   return out
+
+
+def legacy_streams(n_steps, n_obs, y_sigma_alpha, seeds=None, step0=0):
+  """The standard draws the reference's cond_reg consumes, [n_steps, N]:
+  standard_gamma(alpha + n/2) on y_sigma steps, gauss otherwise (NumPy's
+  legacy normal/gamma = loc + scale * gauss / scale * standard_gamma).  With
+  seeds=None: one chain on NumPy's GLOBAL stream, advanced exactly as the
+  reference advances it; otherwise one RandomState(seed) per chain."""
+  alpha = y_sigma_alpha + 0.5 * n_obs
+  gens = [np.random] if seeds is None else \
+      [np.random.RandomState(int(s)) for s in seeds]
+  out = np.empty((n_steps, len(gens)), np.float64)
+  for c, g in enumerate(gens):
+    for t in range(n_steps):
+      out[t, c] = g.standard_gamma(alpha) if (step0 + t) % 3 == 2 \
+          else g.standard_normal()
+  return out
+
+
+def identify_loglik(prob, x_obs, y_obs, n_probe=3):
+  """True when the user density equals norm.logpdf(y, b0 + b1 x, y_sigma)
+  elementwise (gibbs_linreg.py:31-32) at random parameter points: the
+  kernel's v.prob form."""
+  import scipy.stats
+  rs = np.random.RandomState(12345)
+  for _ in range(n_probe):
+    b0, b1 = rs.uniform(-3, 3, size=2)
+    sg = rs.uniform(0.1, 3.)
+    try:
+      got = np.asarray(prob(x=x_obs, y=y_obs, beta_0=b0, beta_1=b1,
+                            y_sigma=sg), np.float64)
+    except Exception:   # noqa: BLE001 -- any failure means "not this form"
+      return False
+    want = scipy.stats.norm.logpdf(y_obs, loc=b0 + b1 * x_obs, scale=sg)
+    if got.shape != want.shape or not np.allclose(got, want, rtol=1e-12,
+                                                  atol=1e-12):
+      return False
+  return True

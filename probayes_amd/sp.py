@@ -200,7 +200,7 @@ class SP:
     """The kernel spec of this process (probayes_amd/spec.py)."""
     from probayes_amd.spec import make_spec
     if self._tfun is not None:
-      raise L.NotLowerable('user tfun Gibbs (set_tfun) has no kernel')
+      return self._lower_linreg(extra, iid, joint)
     names, rvs = self.keylist, self.roots.rvs
     d = len(names)
     extra = {_key(k): v for k, v in (extra or {}).items()}
@@ -247,6 +247,53 @@ class SP:
                                  via_rf=isinstance(self._tran, RF))
     return make_spec(d, target, proposal, scores=scores, pscale=pscale,
                      tran=tran_spec, prior=prior, ufun=ufun, names=names)
+
+  def _lower_linreg(self, extra, iid, joint):
+    """User-tfun Gibbs (rf.py:413-462): lowered when the paras RF's tfun is
+    a linreg.LinRegConditional over beta_0 & beta_1 & y_sigma with tsteps=1,
+    gibbs scores, and a density equal to norm.logpdf(y, b0 + b1 x, y_sigma)
+    over the iid data in `extra` (examples/mcmc/gibbs_linreg.py)."""
+    from probayes_amd import linreg
+    rf = self._subfield(self._tfun) or self._tfun
+    tf = getattr(rf, 'tfun', None)
+    if tf is None or not isinstance(tf[0], linreg.LinRegConditional):
+      raise L.NotLowerable('user tfun Gibbs has a kernel only for '
+                           'linreg.LinRegConditional (gibbs_linreg.py)')
+    cond, _, tkw = tf
+    if tuple(rf.keylist) != linreg.KEYS or tuple(self.keylist) != linreg.KEYS:
+      raise L.NotLowerable('linreg Gibbs needs paras beta_0 & beta_1 & y_sigma')
+    if int(tkw.get('tsteps') or 0) != 1:
+      raise L.NotLowerable('linreg Gibbs needs tsteps=1')
+    if self._scores != 'gibbs' or not iid:
+      raise L.NotLowerable("linreg Gibbs needs set_scores('gibbs') and iid=True")
+    if self.leafs is None or tuple(self.leafs.keylist) != ('x', 'y'):
+      raise L.NotLowerable('linreg Gibbs needs SP(x & y, paras)')
+    ex = {_key(k): v for k, v in (extra or {}).items()}
+    if 'x,y' in ex:
+      x_obs, y_obs = (np.asarray(v, np.float64) for v in ex['x,y'])
+    elif 'x' in ex and 'y' in ex:
+      x_obs, y_obs = np.asarray(ex['x'], np.float64), np.asarray(ex['y'], np.float64)
+    else:
+      raise L.NotLowerable("linreg Gibbs needs the data as extra {'x,y': ...}")
+    for k, v in (('x', x_obs), ('y', y_obs)):
+      if k not in tkw or not np.array_equal(np.asarray(tkw[k], np.float64), v):
+        raise L.NotLowerable('the tfun data must be the sampler data')
+    if cond.n_obs != len(x_obs):
+      raise L.NotLowerable('LinRegConditional n_obs != the data size')
+    if self._prob is None:
+      raise L.NotLowerable('set_prob() first')
+    prob, pargs, pkw = self._prob
+    pkw = dict(pkw)
+    pscale = pkw.pop('pscale', None)
+    if pargs or pkw or not is_log(pscale) or \
+        not linreg.identify_loglik(prob, x_obs, y_obs):
+      raise L.NotLowerable('linreg Gibbs needs the log density '
+                           'norm.logpdf(y, beta_0 + beta_1*x, y_sigma)')
+    rvs = self.roots.rvs
+    vsets = [tuple(rv.vlims) for rv in rvs] if joint else [(0., 1.)] * 3
+    return {'kind': 'linreg', 'names': list(linreg.KEYS), 'pscale': 'log',
+            'x_obs': x_obs, 'y_obs': y_obs, 'hyper': cond.hyper,
+            'vsets': vsets}
 
   def _lower_delta(self, rvs, names):
     delta, dargs, dkw = self._delta_spec()
@@ -441,6 +488,8 @@ class Sampler:
       return self
     self.spec = self.sp.lower(self.extra, self.iid, self.joint)
     self.pscale = self.spec['pscale']
+    if self.spec.get('kind') == 'linreg':
+      return self._run_linreg()
     eng = Engine(self.spec, device=self.device)
     try:
       eng.init_chains(self._init_array())
@@ -472,6 +521,29 @@ class Sampler:
       self.moments = eng.moments()
     finally:
       eng.close()
+    return self
+
+  def _run_linreg(self):
+    from probayes_amd import linreg
+    sp = self.spec
+    if self.thin != 1:
+      raise L.NotLowerable('linreg Gibbs records every step (thin=1)')
+    rand, rng = None, self.rng
+    n_obs = len(sp['x_obs'])
+    if rng == 'legacy':
+      if self.batched and self.seeds is None:
+        raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
+      rand = linreg.legacy_streams(self.stop, n_obs, sp['hyper'][4],
+                                   None if self.seeds is None else self.seeds)
+      rng = 'replay'
+    out = linreg.run(sp['x_obs'], sp['y_obs'], self._init_array(), self.stop,
+                     hyper=sp['hyper'], vsets=sp['vsets'], rng=rng,
+                     seed=self.seed, rand=rand, device=self.device)
+    vx, vp = out['v_x'], out['v_p']
+    # gibbs: p = v, u = True, s = t = None (sp_utils.py:75-84)
+    self.tr = {'v_x': vx, 'v_p': vp, 'p_x': vx, 'p_p': vp,
+               'u': np.ones(vp.shape, np.uint8)}
+    self.moments = None
     return self
 
   def __iter__(self):

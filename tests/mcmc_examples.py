@@ -369,7 +369,9 @@ def gibbs_linreg(pb, params):
 
   stats = x & y
   paras = beta_0 & beta_1 & y_sigma
-  paras.set_tfun(linreg_cond(x_obs, y_obs), tsteps=1, x=x_obs, y=y_obs)
+  cond = params['cond'](len(x_obs)) if 'cond' in params else \
+      linreg_cond(x_obs, y_obs)
+  paras.set_tfun(cond, tsteps=1, x=x_obs, y=y_obs)
   process = pb.SP(stats, paras)
   process.set_tfun(paras)
   process.set_prob(norm_reg, pscale='log')

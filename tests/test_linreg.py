@@ -136,3 +136,69 @@ def test_posterior_matches_oracle_within_monte_carlo_error():
     sd = r[:, -1, k].std()
     assert abs(gm - rm) <= 5 * sd * np.sqrt(1 / n_gpu + 1 / n_cpu), (k, gm, rm)
     assert abs(g[:, -1, k].std() / sd - 1) <= 0.1, k
+
+
+def _facade(root, cond=None):
+  import probayes_amd as pb
+  from mcmc_examples import TFUN_WORKLOADS
+  builder, params, n, t, seed0 = TFUN_WORKLOADS['gibbs_linreg']
+  g, x, y, _ = _golden(root)
+  params = dict(params, x_obs=x, y_obs=y)
+  if cond is not None:
+    params['cond'] = cond
+  return builder(pb, params) + (g, t)
+
+
+def test_facade_lowers_the_descriptor_and_refuses_other_tfuns(root):
+  import probayes_amd as pb
+  process, init, extra, kwds, keys, g, t = _facade(root, linreg.LinRegConditional)
+  spec = process.lower(extra, iid=True, joint=True)
+  assert spec['kind'] == 'linreg' and spec['names'] == list(linreg.KEYS)
+  assert spec['vsets'] == [(-6., 6.), (-6., 6.), (0.001, 10.)]
+  process2, _, extra2, _, _, _, _ = _facade(root)      # a closure cond_reg
+  with pytest.raises(pb.NotLowerable):
+    process2.lower(extra2, iid=True, joint=True)
+  process.set_prob(lambda x, y, beta_0, beta_1, y_sigma: -(y - beta_0) ** 2,
+                   pscale='log')
+  with pytest.raises(pb.NotLowerable):
+    process.lower(extra, iid=True, joint=True)
+
+
+@pytest.mark.gpu
+def test_example_script_reproduces_reference_chain(root):
+  """np.random.seed(s); sampler; walk; SP(samples) as gibbs_linreg.py:74-78
+  does, on NumPy's global stream."""
+  for c in range(2):
+    process, init, extra, kwds, keys, g, t = _facade(
+        root, linreg.LinRegConditional)
+    seed = int(g['seeds'][c])
+    np.random.seed(seed)
+    samples = process.walk(process.sampler(init, extra, stop=t, **kwds))
+    summary = process(samples)
+    for i, k in enumerate(keys):
+      got = np.asarray(summary.v[k])
+      assert np.max(np.abs(got - g['v_x'][c, :, i]) /
+                    np.maximum(np.abs(g['v_x'][c, :, i]), 1.)) <= 1e-12
+    assert np.max(np.abs(np.asarray(summary.v.prob) - g['v_p'][c]) /
+                  np.abs(g['v_p'][c])) <= 1e-12
+    assert summary.u.count(True) == t
+    rs = np.random.RandomState(seed)
+    for s in range(t):
+      rs.standard_gamma(31.) if s % 3 == 2 else rs.standard_normal()
+    assert np.random.random_sample() == rs.random_sample()
+
+
+@pytest.mark.gpu
+def test_batched_sampler_reproduces_all_reference_chains(root):
+  process, init, extra, kwds, keys, g, t = _facade(root, linreg.LinRegConditional)
+  n = len(g['seeds'])
+  sm = process.sampler(init, extra, stop=t, chains=n, seeds=g['seeds'], **kwds)
+  summary = process(process.walk(sm))
+  for i, k in enumerate(keys):
+    got = np.asarray(summary.v[k]).T          # [T, N] -> [N, T]
+    assert np.max(np.abs(got - g['v_x'][:, :, i]) /
+                  np.maximum(np.abs(g['v_x'][:, :, i]), 1.)) <= 1e-12
+  sm = process.sampler(init, extra, stop=t, chains=4096, **kwds)   # philox
+  summary = process(process.walk(sm))
+  assert np.asarray(summary.v['y_sigma']).shape == (t, 4096)
+  assert np.all(np.isfinite(np.asarray(summary.v.prob)))
