@@ -17,9 +17,10 @@
 //   FAST (PHILOX): the sums come from the sufficient statistics Sx, Sy, Sxx,
 //     Sxy, Syy (O(1) per step instead of O(n)); same conditional law.
 // Draws: REPLAY reads the standard gauss / standard_gamma(a + n/2) of each step
-// from rand[T][N]; PHILOX modes draw fp64 Box-Muller normals and
-// Marsaglia-Tsang gammas from Philox-4x32-10 keyed by (seed, global chain),
-// counter (absolute step, attempt).
+// from rand[T][N]; PHILOX modes draw fp64 Box-Muller normals (libm in
+// PHILOX_F64, LDS tables in PHILOX) and Marsaglia-Tsang gammas from
+// Philox-4x32-10 keyed by (seed, global chain), counter (3-step cycle,
+// attempt), so traces do not depend on sharding or launch splits.
 // Trace: x [T][3][N] (chain fastest), lp [T][N]; every step is accepted.
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -66,28 +67,42 @@ __device__ __forceinline__ u32x4 draw_block(const LinregK &a, int64_t gc,
                        (uint32_t)((a.seed >> 32) ^ (uint64_t)(gc >> 32)) + (uint32_t)gc);
 }
 
+// Standard normal pair from one Philox block: libm Box-Muller in the
+// reference-arithmetic modes, the LDS-table form (pbh_device.h) in PHILOX.
+template <bool EXACT>
+__device__ __forceinline__ void normal_pair(u32x4 w, const BMTables *t,
+                                            double &z0, double &z1) {
+  if (EXACT) box_muller(w, z0, z1);
+  else box_muller_tab(w, t, z0, z1);
+}
+
 // Marsaglia & Tsang (2000) for shape a >= 1: d = a - 1/3, c = 1/sqrt(9d);
-// z ~ N(0,1), v = (1 + c z)^3; accept d v when v > 0 and
-// log u < z^2/2 + d - d v + d log v.  Acceptance > 0.98 at the shapes here;
-// every attempt uses a fresh counter, so the loop ends with probability 1
-// (capped at 64 attempts, beyond which the last proposal is returned).
-__device__ __forceinline__ double mt_gamma(const LinregK &a, int64_t gc,
-                                           int64_t step) {
+// z ~ N(0,1), v = (1 + c z)^3; accept d v when v > 0 and u < 1 - 0.0331 z^4
+// (the squeeze, ~98 % of proposals at a = 31, no log) or
+// log u < z^2/2 + d - d v + d log v.  Attempt k of the step's cycle uses the
+// blocks (cycle, k) for z and (cycle, k + 2^16) for u, so the loop ends with
+// probability 1 (capped at 64 attempts, beyond which the last proposal is
+// returned).
+template <bool EXACT>
+__device__ __forceinline__ double mt_gamma(const LinregK &a, const BMTables *tb,
+                                           int64_t gc, int64_t cycle) {
   const double d = a.alpha - 1.0 / 3.0;
   const double c = 1.0 / sqrt(9.0 * d);
   double out = d;
   for (uint32_t att = 1; att <= 64; ++att) {
-    const u32x4 w = draw_block(a, gc, step, att);
     double z, z1;
-    box_muller(u32x4{w.x, w.y, w.z, w.w}, z, z1);
+    normal_pair<EXACT>(draw_block(a, gc, cycle, att), tb, z, z1);
     const double t = 1.0 + c * z;
     if (t <= 0.0) continue;
     const double v = t * t * t;
     out = d * v;
-    // the second deviate's block supplies the uniform
-    const u32x4 w2 = draw_block(a, gc, step, att + 0x10000u);
+    const u32x4 w2 = draw_block(a, gc, cycle, att + 0x10000u);
     const double u = 1.0 - u01(w2.x, w2.y);  // (0, 1]
-    if (log(u) < 0.5 * z * z + d - d * v + d * log(v)) break;
+    const double z2 = z * z;
+    if (u < 1.0 - 0.0331 * (z2 * z2)) break;
+    const double lu = EXACT ? log(u) : fast_log(u);
+    const double lv = EXACT ? log(v) : fast_log(v);
+    if (lu < 0.5 * z2 + d - d * v + d * lv) break;
   }
   return out;
 }
@@ -97,6 +112,8 @@ __global__ void __launch_bounds__(kBlock)
 linreg_gibbs_kernel(LinregK a) {
   extern __shared__ double lds[];
   double *xs = lds, *ys_obs = lds + a.n_obs;
+  __shared__ BMTables s_bmt;
+  if (!EXACT) bm_tables_init(&s_bmt);
   if (EXACT) {
     for (int64_t j = threadIdx.x; j < a.n_obs; j += blockDim.x) {
       xs[j] = a.x_obs[j];
@@ -110,18 +127,26 @@ linreg_gibbs_kernel(LinregK a) {
   const int64_t n = a.n;
   double b0 = a.state[c], b1 = a.state[n + c], sg = a.state[2 * n + c];
   const double nd = (double)a.n_obs;
-  double lp = 0.;
+  double lp = 0., z_next = 0.;
   for (int64_t t = 0; t < a.n_steps; ++t) {
     const int64_t step = a.step0 + t;
     const int key = (int)(step % 3);
+    // Philox draws per 3-step cycle: block (cycle, 0) gives the normals of
+    // the beta_0 and beta_1 steps (z0, z1); the gamma's attempts use their
+    // own blocks.  A launch starting on a beta_1 step recomputes the pair.
     double z;
+    const int64_t cycle = step / 3;
     if (a.mode == PBH_RNG_REPLAY) {
       z = a.rand[t * n + c];
     } else if (key == 2) {
-      z = mt_gamma(a, gc, step);
+      z = mt_gamma<EXACT>(a, &s_bmt, gc, cycle);
+    } else if (key == 0 || t == 0) {
+      double z0, z1;
+      normal_pair<EXACT>(draw_block(a, gc, cycle, 0), &s_bmt, z0, z1);
+      z = key == 0 ? z0 : z1;
+      z_next = z1;
     } else {
-      double z1;
-      box_muller(draw_block(a, gc, step, 0), z, z1);
+      z = z_next;
     }
     if (key == 2) {
       // cond_beta = b + 0.5 * sum((y - b0 - b1 x)**2); 1/sqrt(gamma(a, 1/cb))
@@ -154,7 +179,7 @@ linreg_gibbs_kernel(LinregK a) {
       }
     }
     // v.prob: sum_j norm.logpdf(y_j, b0 + b1 x_j, sg) + the root priors
-    const double lsg = log(sg);
+    const double lsg = EXACT ? log(sg) : fast_log(sg);
     if (EXACT) {
       lp = np_pairwise([&](int64_t j) {
         return lr_norm_logpdf(ys_obs[j], b0 + b1 * xs[j], sg, lsg, a.logC);

@@ -1,5 +1,5 @@
-"""Times the linreg Gibbs kernel (pbh_linreg_gibbs) on one GPU: 65 536 chains
-x 1 000 steps per launch, each RNG mode; prints one JSON line per mode."""
+"""Times the linreg Gibbs kernel (pbh_linreg_gibbs) on one GPU: 65 536 (and
+262 144) chains x 1 000 steps per launch, each RNG mode; prints one JSON line per mode."""
 import json
 import os
 import sys
@@ -10,9 +10,10 @@ from probayes_amd import linreg
 rs = np.random.RandomState(321)
 x = rs.normal(0, 1, size=60)
 y = rs.normal(1.5 * x - 1., 0.5)
-n, t = 65536, 1000
-init = np.tile([-0.9, 1.4, 0.6], (n, 1))
-for rng in ('philox', 'philox_f64', 'replay'):
+t = 1000
+for rng, n in (('philox', 65536), ('philox', 262144), ('philox_f64', 65536),
+               ('replay', 65536)):
+  init = np.tile([-0.9, 1.4, 0.6], (n, 1))
   rand = np.abs(rs.normal(size=(t, n))) + 0.5 if rng == 'replay' else None
   o = linreg.run(x, y, init, t, rng=rng, seed=1, rand=rand, reps=5,
                  trace=False)
