@@ -234,7 +234,9 @@ int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
  * root priors (rf.py:541-562, rv_utils.py:30-38).
  * hyper[6] = beta_0_mu, beta_0_sigma, beta_1_mu, beta_1_sigma,
  *            y_sigma_alpha, y_sigma_beta (cond_reg's keyword defaults);
- * vsets[6] = (lo, hi) of beta_0, beta_1, y_sigma.  Step k of the chain
+ * vsets[6] = closed (lo, hi) of beta_0, beta_1, y_sigma (joint=True: each
+ * adds -log(hi - lo) inside, NEARLY_NEGATIVE_INF outside); NULL = no prior
+ * terms (joint=False).  Step k of the chain
  * (absolute k = step0 + t) updates parameter k mod 3 (the RF's __cond_mod).
  * init/final_x [3][n_chains]; rand [n_steps][n_chains] (REPLAY: the standard
  * gauss, or standard_gamma(alpha + n_obs/2) on y_sigma steps, in NumPy's

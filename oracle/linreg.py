@@ -48,9 +48,19 @@ def linreg_streams(seeds, n_steps, n_obs, hyper=HYPER, cond_mod=0):
   return out
 
 
+NEARLY_NEGATIVE_INF = -1.7976931348623158e+308     # constants.py:31
+
+
 def log_prior(vsets=VSETS):
   """joint=True uniform root priors, added one by one (rv_utils.py:30-38)."""
   return [-np.log(hi - lo) for lo, hi in vsets]
+
+
+def prior_terms(vals, vsets=VSETS):
+  """uniform_prob (rv_utils.py:30-38) per parameter: -log L inside the closed
+  vset, NEARLY_NEGATIVE_INF outside."""
+  return [np.where((v >= lo) & (v <= hi), q, NEARLY_NEGATIVE_INF)
+          for v, (lo, hi), q in zip(vals, vsets, log_prior(vsets))]
 
 
 def loglik(x_obs, y_obs, b0, b1, ys):
@@ -70,7 +80,6 @@ def run_linreg(x_obs, y_obs, init, streams, hyper=HYPER, vsets=VSETS,
   b0, b1, ys = (np.array(init[:, k], np.float64) for k in range(3))
   h = hyper
   sxx = np.sum(x_obs ** 2)
-  pri = log_prior(vsets)
   T, N = streams.shape
   vx = np.empty((N, T, 3))
   vp = np.empty((N, T))
@@ -98,8 +107,10 @@ def run_linreg(x_obs, y_obs, init, streams, hyper=HYPER, vsets=VSETS,
         m = (p1 * h['beta_1_mu'] + yp * s) * v
         b1 = m + np.sqrt(v) * z
     lp = loglik(x_obs, y_obs, b0, b1, ys)
-    for q in pri:
-      lp = lp + q
+    if vsets is not None:
+      with np.errstate(over='ignore'):    # two NEARLY_NEGATIVE_INF -> -inf
+        for q in prior_terms((b0, b1, ys), vsets):
+          lp = lp + q
     vx[:, t, 0], vx[:, t, 1], vx[:, t, 2] = b0, b1, ys
     vp[:, t] = lp
   return {'v_x': vx, 'v_p': vp}

@@ -1164,8 +1164,7 @@ int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
                      double *final_x, double *final_lp, int32_t reps,
                      double *kernel_ms) {
   if (check_ptr(x_obs, "x_obs") || check_ptr(y_obs, "y_obs") ||
-      check_ptr(hyper, "hyper") || check_ptr(vsets, "vsets") ||
-      check_ptr(init, "init"))
+      check_ptr(hyper, "hyper") || check_ptr(init, "init"))
     return PBH_ERR_ARG;
   if (n_obs < 1 || n_obs > pbh::linreg_max_obs())
     return fail(PBH_ERR_ARG, "n_obs must be in 1..%lld, got %lld",
@@ -1196,7 +1195,19 @@ int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
   h.hyper[2] = 1. / (hyper[3] * hyper[3]); h.hyper[3] = hyper[2];
   h.hyper[4] = alpha_post; h.hyper[5] = hyper[5];
   h.hyper[6] = np_pairwise_host(sq.data(), n_obs);
-  for (int k = 0; k < 3; ++k) h.hyper[7 + k] = -std::log(vsets[2 * k + 1] - vsets[2 * k]);
+  for (int k = 0; k < 3; ++k) {
+    if (vsets) {
+      if (!(vsets[2 * k] < vsets[2 * k + 1]))
+        return fail(PBH_ERR_ARG, "vsets[%d] must have lo < hi", k);
+      h.hyper[7 + k] = -std::log(vsets[2 * k + 1] - vsets[2 * k]);
+      h.bounds[2 * k] = vsets[2 * k];
+      h.bounds[2 * k + 1] = vsets[2 * k + 1];
+    } else {            // joint=False: no prior terms (lp + 0.0 == lp)
+      h.hyper[7 + k] = 0.;
+      h.bounds[2 * k] = -HUGE_VAL;
+      h.bounds[2 * k + 1] = HUGE_VAL;
+    }
+  }
   h.hyper[10] = std::log(std::sqrt(2. * M_PI));
   h.stats[0] = sx; h.stats[1] = sy; h.stats[2] = sxy; h.stats[3] = syy;
   h.n_obs = n_obs; h.n = n_chains; h.chain_offset = chain_offset;

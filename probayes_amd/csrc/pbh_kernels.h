@@ -128,7 +128,7 @@ hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
 struct LinregArgs {
   const double *x_obs, *y_obs;
   int64_t n_obs;
-  double hyper[11], stats[4];
+  double hyper[11], stats[4], bounds[6];  // bounds: (lo, hi) per parameter
   double *state, *lp_state;
   const double *rand;
   double *tx, *tp;

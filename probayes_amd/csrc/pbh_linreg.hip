@@ -50,6 +50,7 @@ struct LinregK {
   // Sx, Sy, Sxy, Syy (FAST only)
   double p0, m0, p1, m1, alpha, beta, sxx, pri0, pri1, pri2, logC;
   double sx, sy, sxy, syy;
+  double lo0, hi0, lo1, hi1, lo2, hi2;  // closed vsets of the root priors
   double *state;          // [3][n] beta_0, beta_1, y_sigma (in/out)
   double *lp_state;       // [n] (out)
   const double *rand;     // REPLAY [T][n]
@@ -189,7 +190,12 @@ linreg_gibbs_kernel(LinregK a) {
                         2.0 * b0 * a.sy - 2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
       lp = -0.5 * ss / (sg * sg) - nd * (a.logC + lsg);
     }
-    lp = ((lp + a.pri0) + a.pri1) + a.pri2;
+    // uniform_prob (rv_utils.py:30-38): -log L inside the vset, else
+    // NEARLY_NEGATIVE_INF; added one parameter at a time
+    const double q0 = (b0 >= a.lo0 && b0 <= a.hi0) ? a.pri0 : kNearlyNegInf;
+    const double q1 = (b1 >= a.lo1 && b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
+    const double q2 = (sg >= a.lo2 && sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
+    lp = ((lp + q0) + q1) + q2;
     double *tx = a.tx + t * 3 * n;
     __builtin_nontemporal_store(b0, tx + c);
     __builtin_nontemporal_store(b1, tx + n + c);
@@ -213,6 +219,8 @@ hipError_t launch_linreg_gibbs(const LinregArgs &h, hipStream_t s) {
   a.alpha = h.hyper[4]; a.beta = h.hyper[5]; a.sxx = h.hyper[6];
   a.pri0 = h.hyper[7]; a.pri1 = h.hyper[8]; a.pri2 = h.hyper[9];
   a.logC = h.hyper[10];
+  a.lo0 = h.bounds[0]; a.hi0 = h.bounds[1]; a.lo1 = h.bounds[2];
+  a.hi1 = h.bounds[3]; a.lo2 = h.bounds[4]; a.hi2 = h.bounds[5];
   a.sx = h.stats[0]; a.sy = h.stats[1]; a.sxy = h.stats[2]; a.syy = h.stats[3];
   a.state = h.state; a.lp_state = h.lp_state; a.rand = h.rand;
   a.tx = h.tx; a.tp = h.tp;

@@ -67,7 +67,8 @@ def run(x_obs, y_obs, init, n_steps, hyper=(0., 1., 0., 1., 1., 1.),
   """Runs N chains for n_steps on the GPU.  init [N, 3] (beta_0, beta_1,
   y_sigma).  rng 'replay' reads rand [n_steps, N] (standard draws in NumPy's
   legacy order); 'philox' (fast sufficient-statistics form) and 'philox_f64'
-  (reference arithmetic) draw on the device.  Returns a dict with v_x
+  (reference arithmetic) draw on the device.  vsets: closed (lo, hi) of the
+  joint=True root priors, None for none.  Returns a dict with v_x
   [N, T, 3], v_p [N, T] (when trace), final_x [N, 3], final_p [N] and the
   average kernel ms."""
   x_obs = np.ascontiguousarray(x_obs, np.float64)
@@ -89,7 +90,7 @@ def run(x_obs, y_obs, init, n_steps, hyper=(0., 1., 0., 1., 1., 1.),
   else:
     rand = None
   h = np.asarray(hyper, np.float64)
-  v = np.asarray(vsets, np.float64).reshape(6)
+  v = None if vsets is None else np.asarray(vsets, np.float64).reshape(6)
   init_t = np.ascontiguousarray(init.T)
   tx = np.empty((T, 3, n)) if trace and T else None
   tp = np.empty((T, n)) if trace and T else None

@@ -290,7 +290,9 @@ class SP:
       raise L.NotLowerable('linreg Gibbs needs the log density '
                            'norm.logpdf(y, beta_0 + beta_1*x, y_sigma)')
     rvs = self.roots.rvs
-    vsets = [tuple(rv.vlims) for rv in rvs] if joint else [(0., 1.)] * 3
+    if joint and not all(rv.lo_incl and rv.hi_incl for rv in rvs):
+      raise L.NotLowerable('linreg Gibbs priors need closed (list) vsets')
+    vsets = [tuple(rv.vlims) for rv in rvs] if joint else None
     return {'kind': 'linreg', 'names': list(linreg.KEYS), 'pscale': 'log',
             'x_obs': x_obs, 'y_obs': y_obs, 'hyper': cond.hyper,
             'vsets': vsets}

@@ -155,6 +155,7 @@ def test_facade_lowers_the_descriptor_and_refuses_other_tfuns(root):
   spec = process.lower(extra, iid=True, joint=True)
   assert spec['kind'] == 'linreg' and spec['names'] == list(linreg.KEYS)
   assert spec['vsets'] == [(-6., 6.), (-6., 6.), (0.001, 10.)]
+  assert process.lower(extra, iid=True, joint=False)['vsets'] is None
   process2, _, extra2, _, _, _, _ = _facade(root)      # a closure cond_reg
   with pytest.raises(pb.NotLowerable):
     process2.lower(extra2, iid=True, joint=True)
@@ -202,3 +203,28 @@ def test_batched_sampler_reproduces_all_reference_chains(root):
   summary = process(process.walk(sm))
   assert np.asarray(summary.v['y_sigma']).shape == (t, 4096)
   assert np.all(np.isfinite(np.asarray(summary.v.prob)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('vsets', [None, ((-1., -0.95), (1.3, 1.6), (0.4, 0.62))])
+def test_replay_priors_and_vset_bounds_match_oracle(vsets):
+  """joint=False (no prior) and tight vsets the chains leave: the
+  NEARLY_NEGATIVE_INF terms of uniform_prob (rv_utils.py:30-38)."""
+  x, y = _data(60)
+  n, t = 130, 60
+  init = np.tile([-0.98, 1.45, 0.5], (n, 1))
+  st = linreg_streams(np.arange(300, 300 + n), t, 60)
+  ref = run_linreg(x, y, init, st, vsets=vsets)
+  out = linreg.run(x, y, init, t, rng='replay', rand=st, vsets=vsets)
+  rel = np.abs(out['v_x'] - ref['v_x']) / np.maximum(np.abs(ref['v_x']), 1.)
+  assert rel.max() <= 1e-12
+  fin = np.isfinite(ref['v_p'])
+  assert np.array_equal(fin, np.isfinite(out['v_p']))
+  assert np.array_equal(ref['v_p'][~fin], out['v_p'][~fin])
+  big = np.abs(ref['v_p']) > 1e300
+  assert np.array_equal(big, np.abs(out['v_p']) > 1e300)
+  if vsets is not None:
+    assert big.any() and not big.all()
+  ok = fin & ~big
+  assert np.max(np.abs(out['v_p'][ok] - ref['v_p'][ok]) /
+                np.abs(ref['v_p'][ok])) <= 1e-12
