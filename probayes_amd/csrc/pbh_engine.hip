@@ -1212,6 +1212,12 @@ int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
   h.stats[0] = sx; h.stats[1] = sy; h.stats[2] = sxy; h.stats[3] = syy;
   h.n_obs = n_obs; h.n = n_chains; h.chain_offset = chain_offset;
   h.n_steps = n_steps; h.step0 = step0; h.seed = seed; h.mode = rng_mode;
+  {
+    // the lane-pair kernel is measured slower (1.60 vs 1.22 ms at 65 536
+    // chains x 1 000 steps); PBH_LINREG_PAIR=1 selects it for A/B runs
+    const char *p_env = std::getenv("PBH_LINREG_PAIR");
+    h.pair = p_env && p_env[0] == '1';
+  }
   if (kernel_ms) *kernel_ms = 0.;
   HIP_TRY(hipSetDevice(device));
   const int64_t T = n_steps, N = n_chains;

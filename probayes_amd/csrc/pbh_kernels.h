@@ -135,6 +135,7 @@ struct LinregArgs {
   int64_t n, chain_offset, n_steps, step0;
   uint64_t seed;
   int32_t mode;
+  int32_t pair;   // PHILOX: one chain per lane pair (linreg_pair_kernel)
 };
 int64_t linreg_max_obs();
 hipError_t launch_linreg_gibbs(const LinregArgs &a, hipStream_t s);

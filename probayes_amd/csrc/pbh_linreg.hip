@@ -208,6 +208,148 @@ linreg_gibbs_kernel(LinregK a) {
   a.lp_state[c] = lp;
 }
 
+// FAST arithmetic of one step (the same expressions as the FAST branches of
+// linreg_gibbs_kernel, so both kernels give identical chains).
+__device__ __forceinline__ void fast_step(const LinregK &a, int key, double z,
+                                          double nd, double &b0, double &b1,
+                                          double &sg, double &lp) {
+  if (key == 2) {
+    const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx - 2.0 * b0 * a.sy -
+                      2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
+    const double cb = a.beta + 0.5 * ss;
+    sg = 1.0 / sqrt((1.0 / cb) * z);
+  } else {
+    const double yp = 1.0 / (sg * sg);
+    if (key == 0) {
+      const double v = 1.0 / (a.p0 + nd * yp);
+      const double s = a.sy - b1 * a.sx;
+      const double m = (a.p0 * a.m0 + yp * s) * v;
+      b0 = m + sqrt(v) * z;
+    } else {
+      const double v = 1.0 / (a.p1 + yp * a.sxx);
+      const double s = a.sxy - b0 * a.sx;
+      const double m = (a.p1 * a.m1 + yp * s) * v;
+      b1 = m + sqrt(v) * z;
+    }
+  }
+  const double lsg = fast_log(sg);
+  const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx -
+                    2.0 * b0 * a.sy - 2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
+  lp = -0.5 * ss / (sg * sg) - nd * (a.logC + lsg);
+  const double q0 = (b0 >= a.lo0 && b0 <= a.hi0) ? a.pri0 : kNearlyNegInf;
+  const double q1 = (b1 >= a.lo1 && b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
+  const double q2 = (sg >= a.lo2 && sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
+  lp = ((lp + q0) + q1) + q2;
+}
+
+__device__ __forceinline__ void lr_halves(double v, double &lo, double &hi) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto x = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto y = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  lo = __builtin_bit_cast(double, (uint64_t)x[0] | ((uint64_t)y[0] << 32));
+  hi = __builtin_bit_cast(double, (uint64_t)x[1] | ((uint64_t)y[1] << 32));
+}
+
+// PHILOX production kernel with one chain per lane PAIR (l, l + 32): 65 536
+// chains fill 2 048 wavefronts (2 per SIMD) instead of 1 024.  The draws of
+// a 3-step cycle are split over the halves with one instruction stream: each
+// half forms one Philox block and one Box-Muller pair -- half 0 the beta
+// normals (block (cycle, 0)), half 1 the first Marsaglia-Tsang attempt
+// (blocks (cycle, 1) and (cycle, 1 + 2^16)); the rare rejected attempts
+// continue in mt_gamma.  Two v_permlane32_swap exchanges give every lane the
+// cycle's three draws; both halves then carry the O(1) state update and split
+// the stores (half 0: beta_0, beta_1; half 1: y_sigma, lp).  Draws and
+// arithmetic equal linreg_gibbs_kernel<false>'s, so the chains are identical.
+// Measured slower (1.60 vs 1.22 ms at 65 536 chains x 1 000 steps): the
+// gamma half diverges from the normal half and both halves repeat the fp64
+// update, which outweighs the second wavefront per SIMD.  Off by default
+// (PBH_LINREG_PAIR=1).
+__global__ void __launch_bounds__(kBlock)
+linreg_pair_kernel(LinregK a) {
+  __shared__ BMTables s_bmt;
+  bm_tables_init(&s_bmt);
+  const int lane = threadIdx.x & 63;
+  const bool hi = lane >= 32;
+  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x - lane) / 2 +
+                    (lane & 31);
+  const bool live = c < a.n;            // dead lanes still join the swaps
+  const int64_t cc = live ? c : 0;
+  const int64_t gc = a.chain_offset + cc;
+  const int64_t n = a.n;
+  double b0 = a.state[cc], b1 = a.state[n + cc], sg = a.state[2 * n + cc];
+  const double nd = (double)a.n_obs;
+  const double d = a.alpha - 1.0 / 3.0;
+  const double cm = 1.0 / sqrt(9.0 * d);
+  double lp = 0., z0 = 0., z1 = 0., g = 0.;
+  for (int64_t t = 0; t < a.n_steps; ++t) {
+    const int64_t step = a.step0 + t;
+    const int key = (int)(step % 3);
+    const int64_t cycle = step / 3;
+    if (key == 0 || t == 0) {
+      double p0, p1;
+      normal_pair<false>(draw_block(a, gc, cycle, hi ? 1u : 0u), &s_bmt, p0, p1);
+      double gv = p0;
+      if (hi) {
+        // attempt 1 of mt_gamma, then the rest of its loop if rejected
+        const double tt = 1.0 + cm * p0;
+        bool done = false;
+        if (tt > 0.0) {
+          const double v = tt * tt * tt;
+          gv = d * v;
+          const u32x4 w2 = draw_block(a, gc, cycle, 1u + 0x10000u);
+          const double u = 1.0 - u01(w2.x, w2.y);
+          const double z2 = p0 * p0;
+          done = u < 1.0 - 0.0331 * (z2 * z2) ||
+                 fast_log(u) < 0.5 * z2 + d - d * v + d * fast_log(v);
+        }
+        if (!done) {
+          double out = tt > 0.0 ? gv : d;
+          for (uint32_t att = 2; att <= 64; ++att) {
+            double z, zz;
+            normal_pair<false>(draw_block(a, gc, cycle, att), &s_bmt, z, zz);
+            const double t2 = 1.0 + cm * z;
+            if (t2 <= 0.0) continue;
+            const double v = t2 * t2 * t2;
+            out = d * v;
+            const u32x4 w3 = draw_block(a, gc, cycle, att + 0x10000u);
+            const double u = 1.0 - u01(w3.x, w3.y);
+            const double z2 = z * z;
+            if (u < 1.0 - 0.0331 * (z2 * z2)) break;
+            if (fast_log(u) < 0.5 * z2 + d - d * v + d * fast_log(v)) break;
+          }
+          gv = out;
+        }
+      }
+      double lo_v, hi_v, lo_w, hi_w;
+      lr_halves(gv, lo_v, hi_v);
+      lr_halves(p1, lo_w, hi_w);
+      z0 = lo_v; g = hi_v; z1 = lo_w;
+      (void)hi_w;
+    }
+    const double z = key == 0 ? z0 : (key == 1 ? z1 : g);
+    fast_step(a, key, z, nd, b0, b1, sg, lp);
+    if (live) {
+      double *tx = a.tx + t * 3 * n;
+      if (!hi) {
+        __builtin_nontemporal_store(b0, tx + c);
+        __builtin_nontemporal_store(b1, tx + n + c);
+      } else {
+        __builtin_nontemporal_store(sg, tx + 2 * n + c);
+        __builtin_nontemporal_store(lp, a.tp + t * n + c);
+      }
+    }
+  }
+  if (live) {
+    if (!hi) {
+      a.state[c] = b0;
+      a.state[n + c] = b1;
+    } else {
+      a.state[2 * n + c] = sg;
+      a.lp_state[c] = lp;
+    }
+  }
+}
+
 }  // namespace
 
 int64_t linreg_max_obs() { return 8192; }  // 2 x 8192 x 8 B = 128 KB of LDS
@@ -227,7 +369,10 @@ hipError_t launch_linreg_gibbs(const LinregArgs &h, hipStream_t s) {
   a.n = h.n; a.chain_offset = h.chain_offset; a.n_steps = h.n_steps;
   a.step0 = h.step0; a.seed = h.seed; a.mode = h.mode;
   const dim3 grid((unsigned)((h.n + kBlock - 1) / kBlock)), block(kBlock);
-  if (h.mode == PBH_RNG_PHILOX) {
+  if (h.mode == PBH_RNG_PHILOX && h.pair) {
+    const dim3 grid2((unsigned)((2 * h.n + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL(linreg_pair_kernel, grid2, block, 0, s, a);
+  } else if (h.mode == PBH_RNG_PHILOX) {
     hipLaunchKernelGGL(linreg_gibbs_kernel<false>, grid, block, 0, s, a);
   } else {
     const size_t lds = (size_t)(2 * h.n_obs) * sizeof(double);

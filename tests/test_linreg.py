@@ -228,3 +228,22 @@ def test_replay_priors_and_vset_bounds_match_oracle(vsets):
   ok = fin & ~big
   assert np.max(np.abs(out['v_p'][ok] - ref['v_p'][ok]) /
                 np.abs(ref['v_p'][ok])) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_lane_pair_kernel_equals_one_lane_kernel(monkeypatch):
+  """PBH_LINREG_PAIR=1 runs linreg_pair_kernel (one chain per lane pair);
+  the default PHILOX path runs the one-lane kernel.  Same draws and arithmetic: identical chains,
+  including a ragged chain count and a launch starting mid-cycle."""
+  x, y = _data(60)
+  n, t = 1000 + 13, 77
+  init = np.tile([-0.9, 1.4, 0.6], (n, 1))
+  for step0 in (0, 1, 2):
+    a = linreg.run(x, y, init, t, rng='philox', seed=8, step0=step0)
+    monkeypatch.setenv('PBH_LINREG_PAIR', '1')
+    b = linreg.run(x, y, init, t, rng='philox', seed=8, step0=step0)
+    monkeypatch.delenv('PBH_LINREG_PAIR')
+    assert np.array_equal(a['v_x'], b['v_x'])
+    assert np.array_equal(a['v_p'], b['v_p'])
+    assert np.array_equal(a['final_x'], b['final_x'])
+    assert np.array_equal(a['final_p'], b['final_p'])
