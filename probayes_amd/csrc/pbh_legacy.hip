@@ -51,17 +51,40 @@ struct Mt {
 
   __device__ __forceinline__ uint32_t &k(int i) { return key[(int64_t)i * n + c]; }
 
-  // mt19937_gen: the reference order (later words read updated ones)
+  // mt19937_gen in the reference order (later words read updated ones),
+  // in chunks of kB words whose loads are all issued before the chunk's
+  // stores: a chunk reads k[i+1 .. i+kB] (old values, read before they are
+  // overwritten, as in the sequential loop) and k[j] with j = i + 397 (not yet
+  // written) or j = i - 227 (written by an earlier chunk since kB <= 227), so
+  // the result is the sequential one while kB loads are in flight instead of
+  // one.  The chunk grid splits at 227 = N - M (where j wraps) and at 623.
+  // 98 -> 29 ms for the cfg2-width 250-step streams (kB = 16).
+  static constexpr int kB = 16;
+  __device__ __forceinline__ void twist_chunk(int i0, int cnt) {
+    uint32_t nx[kB + 1], src[kB];
+#pragma unroll
+    for (int u = 0; u <= kB; ++u)
+      if (u <= cnt) nx[u] = k(i0 + u);
+#pragma unroll
+    for (int u = 0; u < kB; ++u)
+      if (u < cnt) {
+        const int i = i0 + u;
+        src[u] = k(i < kN - kM ? i + kM : i + kM - kN);
+      }
+#pragma unroll
+    for (int u = 0; u < kB; ++u)
+      if (u < cnt) {
+        const uint32_t y = (nx[u] & kUpper) | (nx[u + 1] & kLower);
+        k(i0 + u) = src[u] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+      }
+  }
+
   __device__ void twist() {
-    uint32_t cur = k(0);
-    for (int i = 0; i < kN - 1; ++i) {
-      const uint32_t nxt = k(i + 1);
-      const uint32_t y = (cur & kUpper) | (nxt & kLower);
-      const int j = i < kN - kM ? i + kM : i + kM - kN;
-      k(i) = k(j) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-      cur = nxt;
-    }
-    const uint32_t y = (cur & kUpper) | (k(0) & kLower);
+    for (int i = 0; i < kN - kM; i += kB)          // [0, 227)
+      twist_chunk(i, (kN - kM) - i < kB ? (kN - kM) - i : kB);
+    for (int i = kN - kM; i < kN - 1; i += kB)     // [227, 623)
+      twist_chunk(i, (kN - 1) - i < kB ? (kN - 1) - i : kB);
+    const uint32_t y = (k(kN - 1) & kUpper) | (k(0) & kLower);
     k(kN - 1) = k(kM - 1) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
     pos = 0;
   }
