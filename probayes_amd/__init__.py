@@ -16,3 +16,5 @@ from probayes_amd.lower import NotLowerable  # noqa: F401,E402
 from probayes_amd import models  # noqa: F401,E402
 from probayes_amd import likelihoods  # noqa: F401,E402
 from probayes_amd.likelihoods import bool_perm_freq  # noqa: F401,E402
+from probayes_amd import linreg  # noqa: F401,E402
+from probayes_amd.linreg import LinRegConditional  # noqa: F401,E402
