@@ -151,11 +151,45 @@ def bench_legacy_replay():
           'config': 'cfg2 shape, REPLAY mode fed by pbh_legacy_replay'}
 
 
+def bench_linreg(cpu, budget_s):
+  """gibbs_linreg user-conditional Gibbs (60 observations), PHILOX:
+  65 536 chains x 1 000 coordinate steps per launch, full trace on device."""
+  from oracle.linreg import linreg_streams, run_linreg
+  from probayes_amd import linreg
+  rs = np.random.RandomState(321)
+  x = rs.normal(0, 1, size=60)
+  y = rs.normal(1.5 * x - 1., 0.5)
+  n, t = 65536, 1000
+  init = np.tile([-0.9, 1.4, 0.6], (n, 1))
+  ms = linreg.run(x, y, init, t, rng='philox', seed=1, reps=5,
+                  trace=False)['ms']
+  o = {'workload': 'gibbs_linreg (60 obs) PHILOX', 'chains': n, 'steps': t,
+       'kernel_ms': ms, 'coordinate_steps_per_s': n * t / (ms / 1e3),
+       'roofline': roofline(4 * 8, n * t, ms, 'linreg_gibbs_kernel<false>'),
+       'config': 'user-tfun Gibbs, examples/mcmc/gibbs_linreg.py model'}
+  if cpu:
+    m, tc = 1024, 30
+    done, reps, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+      st = linreg_streams(np.arange(reps * m, (reps + 1) * m), tc, 60)
+      run_linreg(x, y, init[:m], st)
+      done += m * tc
+      reps += 1
+    el = time.perf_counter() - t0
+    o['cpu_baseline'] = {
+        'value': done / el, 'unit': 'coordinate-steps/s', 'cores': 1,
+        'kind': 'port',
+        'sample': '{} chains x {} steps x {} reps through oracle.run_linreg '
+                  'incl. per-chain RandomState streams'.format(m, tc, reps)}
+  return o
+
+
 def main():
   import argparse
   ap = argparse.ArgumentParser()
-  ap.add_argument('--only', default='cfg1,cfg3,cfg5,lik,legacy',
-                  help='comma-separated subset of cfg1,cfg3,cfg5,lik,legacy')
+  ap.add_argument('--only', default='cfg1,cfg3,cfg5,lik,legacy,linreg',
+                  help='comma-separated subset of cfg1,cfg3,cfg5,lik,legacy,'
+                       'linreg')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--cpu-budget', type=float, default=4.0,
                   help='seconds of oracle work per cpu_baseline')
@@ -193,6 +227,8 @@ def main():
     lines.append(bench_bool_perm_freq(cpu, args.cpu_budget))
   if 'legacy' in only:
     lines.append(bench_legacy_replay())
+  if 'linreg' in only:
+    lines.append(bench_linreg(cpu, args.cpu_budget))
   if 'cfg5' not in only:
     for line in lines:
       print(json.dumps(line), flush=True)
