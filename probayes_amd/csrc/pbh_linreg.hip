@@ -129,6 +129,9 @@ linreg_gibbs_kernel(LinregK a) {
   double b0 = a.state[c], b1 = a.state[n + c], sg = a.state[2 * n + c];
   const double nd = (double)a.n_obs;
   double lp = 0., z_next = 0.;
+  // FAST: 1 / sg^2 and log sg change only on y_sigma steps (same values as
+  // recomputing them every step)
+  double yp_c = 1.0 / (sg * sg), lsg_c = EXACT ? 0. : fast_log(sg);
   for (int64_t t = 0; t < a.n_steps; ++t) {
     const int64_t step = a.step0 + t;
     const int key = (int)(step % 3);
@@ -163,8 +166,12 @@ linreg_gibbs_kernel(LinregK a) {
       }
       const double cb = a.beta + 0.5 * ss;
       sg = 1.0 / sqrt((1.0 / cb) * z);
+      if (!EXACT) {
+        yp_c = 1.0 / (sg * sg);
+        lsg_c = fast_log(sg);
+      }
     } else {
-      const double yp = 1.0 / (sg * sg);
+      const double yp = EXACT ? 1.0 / (sg * sg) : yp_c;
       if (key == 0) {
         const double v = 1.0 / (a.p0 + nd * yp);
         const double s = EXACT ? np_pairwise([&](int64_t j) {
@@ -180,7 +187,7 @@ linreg_gibbs_kernel(LinregK a) {
       }
     }
     // v.prob: sum_j norm.logpdf(y_j, b0 + b1 x_j, sg) + the root priors
-    const double lsg = EXACT ? log(sg) : fast_log(sg);
+    const double lsg = EXACT ? log(sg) : lsg_c;
     if (EXACT) {
       lp = np_pairwise([&](int64_t j) {
         return lr_norm_logpdf(ys_obs[j], b0 + b1 * xs[j], sg, lsg, a.logC);
