@@ -36,6 +36,17 @@ D = 10
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+RNG_DESC = {
+    'philox': 'philox4x32-10; fp64 Box-Muller normals on 52-bit uniforms '
+              '(table-driven log/sqrt/sincos, a few ulp from libm)',
+    'philox_f64': 'philox4x32-10; libm fp64 Box-Muller normals, reference '
+                  'arithmetic',
+    'xoshiro': 'xoshiro128** per chain; fp64 Box-Muller normals as philox',
+    'philox_fp32': 'philox4x32-10; fp32 hardware Box-Muller normals on 24-bit '
+                   'uniforms (|z| <= 5.77) -- comparison only, not fp64',
+}
+
+
 def cfg2_spec():
   from probayes_amd.spec import make_spec
   return make_spec(
@@ -77,19 +88,20 @@ def cpu_baseline(budget_s=12.0):
                     'core, BASELINE.md)'.format(n, t, reps)}
 
 
-def measured_traffic(chains, spl, rng, trace):
-  """HBM bytes per launch of this exact launch shape, from the newest
-  profiles/r*_traffic.json (rocprofv3 PMC passes of scripts/profile.sh), or
-  None when no profile matches."""
+def measured_traffic(chains, launch_steps, rng, trace):
+  """HBM bytes per launch of this exact launch shape (chains, steps in the
+  launch, RNG mode), from the newest profiles/r*_traffic.json (rocprofv3 PMC
+  passes, scripts/profile.sh), or None when no profile matches."""
   import glob
   files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic.json')))
-  if not trace or rng != 'philox':
+  if not trace:
     return None
   for path in reversed(files):   # newest profile of this kernel and shape
     with open(path) as f:
       t = json.load(f)
     if (t.get('kernel', '').startswith('mh_pair_kernel') and
-        t.get('chains') == chains and t.get('steps_per_launch') == spl):
+        t.get('chains') == chains and t.get('rng', 'philox_fp32') == rng and
+        t.get('steps_per_launch') == launch_steps):
       return t['bytes_per_launch']
   return None
 
@@ -105,7 +117,10 @@ def main():
   ap.add_argument('--steps-per-launch', type=int, default=250)
   ap.add_argument('--no-trace', action='store_true')
   ap.add_argument('--rng', default='philox',
-                  choices=['philox', 'philox_f64', 'xoshiro'])
+                  choices=['philox', 'philox_f64', 'xoshiro', 'philox_fp32'])
+  ap.add_argument('--moments', action='store_true',
+                  help='keep in-kernel running moments (off: the trace is '
+                  'reduced on the device after the timed region)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--traffic-bytes', type=float, default=None,
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
@@ -125,6 +140,7 @@ def main():
   offset, n = shard(n * world, rank, world)   # weak scaling: n chains / GPU
   eng.init_chains(np.zeros((n, D)), chain_offset=offset)
   eng.set_rng(args.rng, seed=20261015)
+  eng.set_collect(moments=args.moments or args.no_trace)
   if not args.no_trace:
     eng.alloc_trace(args.warmup + args.steps, 1)
 
@@ -154,6 +170,8 @@ def main():
   if world > 1:
     el = eng.rccl_allreduce_max(el)
     t1 = time.perf_counter()
+    if not args.no_trace and not args.moments:
+      eng.trace_stats(args.warmup, args.steps)   # device reduction of the trace
     eng.rccl_allgather_moments()
     collect_ms = (time.perf_counter() - t1) * 1e3
   else:
@@ -170,26 +188,23 @@ def main():
         'metric': METRIC, 'value': value, 'unit': 'chain-steps/s',
         'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': el * 1e3 / args.steps, 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
+        'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'f32 normals, f64 chain' if args.rng == 'philox_fp32' else 'f64',
         'data': 'synthetic',
         'config': {'workload': 'cfg2: 10-dim diagonal-Gaussian random-walk '
                                'MH, {} chains/GPU, full trace every step'
                                .format(n),
                    'chains_per_gpu': n, 'dim': D,
-                   'rng': {'philox': 'philox4x32-10, fp32 Box-Muller normals '
-                                     'with exact sign symmetry',
-                           'philox_f64': 'philox4x32-10, fp64 Box-Muller normals',
-                           'xoshiro': 'xoshiro128** per chain, fp32 Box-Muller '
-                                      'normals with exact sign symmetry'
-                           }[args.rng],
+                   'rng': RNG_DESC[args.rng],
                    'trace': not args.no_trace, 'steps_per_launch': spl,
                    'parallelism': 'chain-sharded x{}'.format(world)},
         'roofline': {'bound': 'hbm', 'achieved': achieved,
                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS,
                      'traffic': args.traffic_bytes if args.traffic_bytes
-                                else measured_traffic(n, spl, args.rng,
-                                                      not args.no_trace),
+                                else measured_traffic(
+                                    n, min(spl, args.steps), args.rng,
+                                    not args.no_trace),
                      'bytes_per_chain_step': bpcs,
                      'kernel': ('mh_pair_kernel<10, {}>' if not os.environ.get('PBH_NO_PAIR') else 'mh_kernel<10, {}, DIAG, GAUSS>').format(args.rng.upper()),
                      'avg_launch_ms': avg_launch_s * 1e3,

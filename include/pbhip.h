@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PBH_ABI_VERSION 2
+#define PBH_ABI_VERSION 3
 #define PBH_MAX_DIM 32
 
 #define PBH_OK 0
@@ -61,13 +61,23 @@ enum pbh_rng_mode {
   PBH_RNG_REPLAY = 0,    /* randoms read from a caller-supplied [T][R][N]
                             stream; reference arithmetic (parity mode)        */
   PBH_RNG_PHILOX = 1,    /* production: Philox-4x32-10 keyed by (seed, global
-                            chain id); fp32 Box-Muller normals with exact sign
-                            symmetry, FMA-corrected divisions                 */
-  PBH_RNG_PHILOX_F64 = 2, /* Philox-4x32-10 with fp64 Box-Muller normals and
-                            the reference arithmetic of REPLAY                 */
-  PBH_RNG_XOSHIRO = 3    /* production, fastest: one xoshiro128** stream per
-                            chain (per lane half), seeded by SplitMix64 of
-                            (seed, global chain id); otherwise as PHILOX      */
+                            chain id); fp64 Box-Muller normals on 52-bit
+                            uniforms (table-driven log / sqrt / sincos, a few
+                            ulp from libm), fp64 chain arithmetic in the
+                            production (FMA) forms                            */
+  PBH_RNG_PHILOX_F64 = 2, /* Philox-4x32-10 with libm fp64 Box-Muller normals
+                            and the reference arithmetic of REPLAY             */
+  PBH_RNG_XOSHIRO = 3,   /* production: one xoshiro128** stream per chain (per
+                            lane half), seeded by SplitMix64 of (seed, global
+                            chain id); otherwise as PHILOX                    */
+  PBH_RNG_PHILOX_FP32 = 4 /* comparison only (the round-1 production form):
+                            as PHILOX but fp32 hardware Box-Muller normals on
+                            24-bit uniforms (|z| <= 5.77) with exact sign
+                            symmetry; lane-pair diagonal-Gauss kernel only   */
+};
+/* What pbh_run accumulates besides the trace (pbh_set_collect). */
+enum pbh_collect {
+  PBH_COLLECT_MOMENTS = 1   /* per-chain sum / sumsq / n_acc (pbh_get_moments) */
 };
 
 /* Joint density + acceptance (replaces RF.set_prob/set_tran + SP.set_scores:
@@ -183,6 +193,10 @@ int pbh_alloc_trace(pbh_engine *eng, int64_t capacity, int32_t thin,
  * steps_per_launch bounds one kernel's fused step loop (0 = all).          */
 int pbh_run(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
 int pbh_sync(pbh_engine *eng);
+/* flags = OR of enum pbh_collect; default PBH_COLLECT_MOMENTS.  With 0 the
+ * kernels keep no running moments (no per-launch read-modify-write of them);
+ * pbh_trace_stats then reduces the recorded trace on the device instead.   */
+int pbh_set_collect(pbh_engine *eng, int32_t flags);
 /* Kernel-only time of the last pbh_run (HIP events on the engine stream). */
 int pbh_last_run_ms(pbh_engine *eng, double *ms, int64_t *launches);
 
@@ -200,6 +214,14 @@ int pbh_get_trace(pbh_engine *eng, int64_t first, int64_t n, double *x,
 int pbh_get_moments(pbh_engine *eng, double *sum, double *sumsq,
                     int64_t *n_acc, int64_t *n_steps);
 int pbh_reset_moments(pbh_engine *eng);
+/* The same per-chain statistics reduced on the device from trace records
+ * [first, first + count) (PD summate + expectation over a recorded trace,
+ * pd_utils.py:332-411, pd.py:373-407, without copying the trace to the
+ * host).  The result replaces the engine's moment buffers (what
+ * pbh_rccl_allgather_moments sends, n_steps = count); host pointers may be
+ * NULL.                                                                     */
+int pbh_trace_stats(pbh_engine *eng, int64_t first, int64_t count, double *sum,
+                    double *sumsq, int64_t *n_acc);
 
 /* ---- multi-GPU: one RCCL all-gather over xGMI --------- */
 int pbh_rccl_unique_id(uint8_t id[128]);
@@ -268,6 +290,14 @@ int pbh_check_accept(int device, int64_t n, const double *lp,
  * words[n][4]; fast[n][2], ref[n][2] receive (z0, z1) of each.             */
 int pbh_check_normals(int device, int64_t n, const uint32_t *words,
                       double *fast, double *ref);
+
+/* The production fp64 normals (bm64_pair, PBH_RNG_PHILOX / XOSHIRO) on n
+ * blocks words[n][4]: fast[n][2] = bm64_pair, ref[n][2] = the same u1 and
+ * angle through libm log / sqrt / sincos.  pbh_bm64_tables fills out[2564]
+ * with the engine's tables ({-2 ln(c_j/2), 1/c_j} x 1025, {sin, cos} x 257). */
+int pbh_check_normals64(int device, int64_t n, const uint32_t *words,
+                        double *fast, double *ref);
+int pbh_bm64_tables(double *out);
 
 #ifdef __cplusplus
 }

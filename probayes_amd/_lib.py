@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PBHIP_LIB', os.path.join(_HERE, 'libpbhip.so'))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_DIM = 32
 
 # enums (pbhip.h)
@@ -21,7 +21,9 @@ PSCALE = {'log': 0, 'lin': 1}
 SCORES = {'hastings': 1, 'metropolis': 2, 'gibbs': 3}
 TRAN = {'const': 1, 'gauss_pdf': 2}
 PROPOSAL = {'gauss': 1, 'sphere': 2, 'uniform': 3, 'gibbs': 4}
-RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2, 'xoshiro': 3}
+RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2, 'xoshiro': 3,
+       'philox_fp32': 4}
+COLLECT_MOMENTS = 1
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
@@ -86,6 +88,7 @@ SIGNATURES = {
                                        ctypes.c_int32, ctypes.c_int32]),
     'pbh_run': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),
     'pbh_sync': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_set_collect': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     'pbh_last_run_ms': (ctypes.c_int, [ctypes.c_void_p, _dp, _i64p]),
     'pbh_get_state': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp]),
     'pbh_trace_len': (ctypes.c_int, [ctypes.c_void_p, _i64p]),
@@ -94,6 +97,8 @@ SIGNATURES = {
                                      _dp]),
     'pbh_get_moments': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp, _i64p, _i64p]),
     'pbh_reset_moments': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_trace_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.c_int64, _dp, _dp, _i64p]),
     'pbh_rccl_unique_id': (ctypes.c_int, [_u8p]),
     'pbh_rccl_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
                                      ctypes.c_int32, _u8p]),
@@ -104,6 +109,9 @@ SIGNATURES = {
                                         _u32p, _u32p, ctypes.c_int32, _u8p]),
     'pbh_check_normals': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _u32p,
                                          _dp, _dp]),
+    'pbh_check_normals64': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _u32p,
+                                           _dp, _dp]),
+    'pbh_bm64_tables': (ctypes.c_int, [_dp]),
     'pbh_bool_perm_freq': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64,
                                           ctypes.c_int32,
                                           ctypes.POINTER(ctypes.c_uint8),

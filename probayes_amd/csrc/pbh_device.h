@@ -218,7 +218,114 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
   z1 = r * s;
 }
 
-// Production normals (PBH_RNG_PHILOX): two standard-normal pairs per Philox
+// ---------------------------------------------------------------------------
+// Production fp64 normals (PBH_RNG_PHILOX, PBH_RNG_XOSHIRO): Box-Muller on
+// two 52-bit uniforms per pair (the reference draws fp64 normals: NumPy's
+// legacy polar gauss on 53-bit uniforms behind scipy norm.rvs,
+// examples/mcmc/mcmc_prob2.py:31).  One 128-bit block (x, y, z, w) gives
+//   u1 = (k1 + 1/2) 2^-52 in (0, 1), k1 = x[19:0]:y   (never 0 or 1),
+//   alpha = (j + k2 2^-52) (pi/2) / 256,  j = z[29:22], k2 = z[19:0]:w,
+//   z0 = s0 r cos(alpha), z1 = s1 r sin(alpha), r = sqrt(-2 ln u1),
+// with the independent sign bits s0 = z[31], s1 = z[30]: reflecting a
+// uniform quarter-turn angle by two fair signs is the uniform full-turn angle
+// exactly.  Spare bits: x[31:20] (12) and z[21:20] (2).
+//   E = -2 ln u1 = (e + 1)(-2 ln 2) - 2 ln(c_j / 2) + r q(r),  c_j = m rounded
+//             to 10 mantissa bits (j in [0, 1024]), r = (m - c_j) / c_j with
+//             one rounding (m - c_j is exact), |r| <= 2^-11, q(r) =
+//             -2 log1p(r) / r to degree 4 (truncation r^5 / 6 < 2^-58
+//             relative); u1 -> 1 takes c = 2 and ln(c/2) = 0, so E keeps its
+//             relative accuracy there;
+//   sqrt    = v_rsq_f64 + two Newton steps;
+//   (sin, cos)(alpha) = table angle j rotated by theta < pi/512: sin degree
+//             5, cos degree 4 (truncations 2e-19 relative, 1e-18 absolute).
+// Tables (host-computed in long double, pbh_dispatch.cpp bm64_tables) live
+// in LDS: 1025 {-2 ln(c_j/2), 1/c_j} pairs and 257 {sin, cos} pairs, 20.5 KB.
+// About 45 VALU per pair.  Accuracy: tests/test_gpu_normals.py (libm form).
+// ---------------------------------------------------------------------------
+constexpr int kBm64LogN = 1025, kBm64ScN = 257;
+constexpr int kBm64Doubles = 2 * (kBm64LogN + kBm64ScN);   // 2564 doubles
+
+__device__ __forceinline__ uint32_t hi32(double v) {
+  return (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32);
+}
+__device__ __forceinline__ uint32_t lo32(double v) {
+  return (uint32_t)__builtin_bit_cast(uint64_t, v);
+}
+__device__ __forceinline__ double from_words(uint32_t hi, uint32_t lo) {
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Copies the global table block (pbh_engine's bm64_tables) into LDS; every
+// thread of the workgroup takes part, then one barrier.
+__device__ __forceinline__ void bm64_load(double *lds, const double *g) {
+  const double2 *src = reinterpret_cast<const double2 *>(g);
+  double2 *dst = reinterpret_cast<double2 *>(lds);
+  for (int i = threadIdx.x; i < kBm64Doubles / 2; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void bm64_pair(uint32_t x, uint32_t y, uint32_t z,
+                                          uint32_t w, const double *tab,
+                                          double &z0, double &z1) {
+  // ---- E = -2 ln u1 ----
+  const double d1 = from_words(0x3FF00000u | (x & 0xFFFFFu), y);   // [1, 2)
+  const double u1 = d1 - (1.0 - 0x1p-53);                          // exact (Sterbenz)
+  const uint32_t uh = hi32(u1);
+  const int e1 = (int)((uh >> 20) & 0x7FFu) - 1022;                // exponent + 1
+  const uint32_t mh = 0x3FF00000u | (uh & 0xFFFFFu);
+  const uint32_t ch = (mh + 0x200u) & 0xFFFFFC00u;                 // c_j (hi word)
+  const double2 lt = reinterpret_cast<const double2 *>(tab)[(ch - 0x3FF00000u) >> 10];
+  const double r = (from_words(mh, lo32(u1)) - from_words(ch, 0u)) * lt.y;
+  double q = __builtin_fma(r, -0.4, 0.5);
+  q = __builtin_fma(q, r, -2.0 / 3.0);
+  q = __builtin_fma(q, r, 1.0);
+  q = __builtin_fma(q, r, -2.0);
+  const double de = (double)e1;
+  const double base = __builtin_fma(de, -2.0 * 6.93147180369123816490e-01,
+                                    __builtin_fma(de, -2.0 * 1.90821492927058770002e-10, lt.x));
+  const double E = __builtin_fma(r, q, base);                       // > 0
+  // ---- sqrt(E): v_rsq_f64 + two Newton steps ----
+  const double yr = __builtin_amdgcn_rsq(E);
+  const double hy = 0.5 * yr;
+  double rr = E * yr;
+  rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
+  rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
+  // ---- (sin, cos) of the quarter-turn angle ----
+  const double2 sc = reinterpret_cast<const double2 *>(tab + 2 * kBm64LogN)[(z >> 22) & 0xFFu];
+  const double d2 = from_words(0x43300000u | (z & 0xFFFFFu), w);    // 2^52 + k2
+  constexpr double kC = 3.14159265358979323846 * 0x1p-61;   // (pi/2) 2^-8 2^-52
+  const double th = __builtin_fma(d2, kC, -kC * 4503599627370496.0);
+  const double f = th * th;
+  const double ps = __builtin_fma(f, 8.3333333333333333333e-03, -1.6666666666666666667e-01);
+  const double st = __builtin_fma(th * f, ps, th);
+  const double ct = __builtin_fma(f, __builtin_fma(f, 4.1666666666666666667e-02, -0.5), 1.0);
+  const double sn = __builtin_fma(sc.x, ct, sc.y * st);
+  const double cs = __builtin_fma(sc.y, ct, -(sc.x * st));
+  const double a0 = rr * cs, a1 = rr * sn;
+  z0 = from_words(hi32(a0) ^ (z & 0x80000000u), lo32(a0));
+  z1 = from_words(hi32(a1) ^ ((z << 1) & 0x80000000u), lo32(a1));
+}
+
+// The 14 spare bits of a bm64_pair block: x[31:20] << 2 | z[21:20].
+__device__ __forceinline__ uint32_t bm64_spare(uint32_t x, uint32_t z) {
+  return ((x >> 20) << 2) | ((z >> 20) & 3u);
+}
+
+// Trace store through a buffer resource: base = a wave-uniform (SGPR)
+// pointer, voff = a loop-invariant per-lane byte offset, soff = a
+// wave-uniform byte offset: no per-store VALU address arithmetic.  nt: the
+// trace is write-once (aux bit 1 = nt on gfx950).
+__device__ __forceinline__ void st_buf(double *base, uint32_t voff,
+                                       uint32_t soff, double v) {
+  typedef unsigned int u32x2_t __attribute__((__vector_size__(8)));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
+                                        (int)voff, (int)soff, 2);
+}
+
+// Legacy fp32 normals (PBH_RNG_PHILOX_FP32, the round-1 production form, kept
+// as a labelled comparison): two standard-normal pairs per Philox
 // block from the hardware fp32 transcendentals (v_log_f32, v_sin_f32,
 // v_cos_f32), widened to fp64.  The magnitude r = sqrt(-2 ln u1) uses 24-bit
 // u1 in (0, 1] (|z| <= 5.77) and the angle lives in one quadrant; each

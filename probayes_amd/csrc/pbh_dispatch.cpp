@@ -1,6 +1,8 @@
 // pbh_dispatch.cpp -- runtime dim -> compiled kernel instantiation.
 // The kernels are instantiated per dimension in pbh_inst_*.hip so that the
 // gfx950 code objects compile in parallel.
+#include <cmath>
+
 #include "pbh_kernels.h"
 #include "pbh_device.h"
 #include "../../include/pbhip.h"
@@ -114,6 +116,94 @@ hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
                                 double *ref) {
   hipLaunchKernelGGL(check_normals_kernel, dim3((unsigned)((n + 255) / 256)),
                      dim3(256), 0, 0, n, words, fast, ref);
+  return hipGetLastError();
+}
+
+// Per-chain sums of a recorded trace [rec][d][n] over records [first, first +
+// count): thread (k, c) walks its column; every wave reads 512 contiguous
+// bytes per record.  Threads k == d count the accept bits of chain c.
+__global__ void trace_stats_kernel(const double *tx, const uint64_t *tacc,
+                                   int64_t n, int32_t d, int64_t W,
+                                   int64_t first, int64_t count, double *sum,
+                                   double *sumsq, int64_t *nacc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = i / n, c = i % n;
+  if (k > d) return;
+  if (k < d) {
+    double s = 0., q = 0.;
+    const double *p = tx + (first * d + k) * n + c;
+    for (int64_t r = 0; r < count; ++r, p += d * n) {
+      const double v = *p;
+      s += v;
+      q = __builtin_fma(v, v, q);
+    }
+    sum[k * n + c] = s;
+    sumsq[k * n + c] = q;
+  } else {
+    int64_t a = 0;
+    const uint64_t *m = tacc + first * W + (c >> 6);
+    for (int64_t r = 0; r < count; ++r, m += W) a += (*m >> (c & 63)) & 1u;
+    nacc[c] = a;
+  }
+}
+
+hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
+                              int32_t d, int64_t W, int64_t first,
+                              int64_t count, double *sum, double *sumsq,
+                              int64_t *nacc, hipStream_t s) {
+  const int64_t m = (int64_t)(d + 1) * n;
+  hipLaunchKernelGGL(trace_stats_kernel, dim3((unsigned)((m + 255) / 256)),
+                     dim3(256), 0, s, tx, tacc, n, d, W, first, count, sum,
+                     sumsq, nacc);
+  return hipGetLastError();
+}
+
+// The bm64 tables (pbh_device.h): {-2 ln(c_j / 2), 1 / c_j} for c_j = 1 + j /
+// 1024, j = 0..1024, then {sin, cos}(j (pi/2) / 256), j = 0..256.  Evaluated
+// in long double (64-bit significand) and rounded once to double.
+void bm64_tables(double *out) {
+  for (int j = 0; j < kBm64LogN; ++j) {
+    const double c = 1.0 + j / 1024.0;   // exact
+    out[2 * j] = (double)(-2.0L * logl((long double)c / 2.0L));
+    out[2 * j + 1] = 1.0 / c;
+  }
+  const long double pi = 3.141592653589793238462643383279502884L;
+  double *sc = out + 2 * kBm64LogN;
+  for (int j = 0; j < kBm64ScN; ++j) {
+    const long double t = pi / 2.0L * (long double)j / 256.0L;
+    sc[2 * j] = (double)sinl(t);
+    sc[2 * j + 1] = (double)cosl(t);
+  }
+  sc[2 * 256] = 1.0;   // sin(pi/2), cos(pi/2) = 0 exactly
+  sc[2 * 256 + 1] = 0.0;
+}
+
+// Diagnostic: bm64_pair against the same construction through ocml's libm
+// log / sqrt / sincos (u1 and the angle formed exactly as bm64_pair forms them).
+__global__ void check_normals64_kernel(int64_t n, const uint32_t *words,
+                                       const double *tab, double *fast,
+                                       double *ref) {
+  __shared__ double s_bmt[kBm64Doubles];
+  bm64_load(s_bmt, tab);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = words[4 * i], y = words[4 * i + 1], z = words[4 * i + 2],
+                 w = words[4 * i + 3];
+  bm64_pair(x, y, z, w, s_bmt, fast[2 * i], fast[2 * i + 1]);
+  const double u1 = from_words(0x3FF00000u | (x & 0xFFFFFu), y) - (1.0 - 0x1p-53);
+  const double k2 = from_words(0x43300000u | (z & 0xFFFFFu), w) - 4503599627370496.0;
+  const double turn = ((double)((z >> 22) & 0xFFu) + k2 * 0x1p-52) * (1.0 / 1024.0);
+  double sv, cv;
+  sincospi(2.0 * turn, &sv, &cv);   // turn of 2 pi
+  const double r = sqrt(-2.0 * log(u1));
+  ref[2 * i] = ((z >> 31) & 1u) ? -(r * cv) : r * cv;
+  ref[2 * i + 1] = ((z >> 30) & 1u) ? -(r * sv) : r * sv;
+}
+
+hipError_t launch_check_normals64(int64_t n, const uint32_t *words,
+                                  const double *tab, double *fast, double *ref) {
+  hipLaunchKernelGGL(check_normals64_kernel, dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, 0, n, words, tab, fast, ref);
   return hipGetLastError();
 }
 

@@ -54,10 +54,14 @@ struct pbh_engine {
   double *tx = nullptr, *tlp = nullptr, *tpx = nullptr, *tpp = nullptr,
          *ts = nullptr;
   uint64_t *tacc = nullptr;
-  // moments
+  // moments (pbh_set_collect)
+  int32_t collect = PBH_COLLECT_MOMENTS;
   double *msum = nullptr, *msq = nullptr;
   int64_t *nacc = nullptr;
   int64_t mom_steps = 0;
+  // production fp64 normal tables (bm64, pbh_device.h), read into LDS
+  double *bm64 = nullptr;
+  bool spin_sync = true;     // PBH_SYNC=block: hipStreamSynchronize instead
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
   bool gibbs_fast = true;    // PBH_GIBBS_FAST=0 keeps the ndtri kernel for Philox
@@ -187,12 +191,21 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gf = std::getenv("PBH_GIBBS_FAST")) e->gibbs_fast = gf[0] != '0';
   if (const char *gl = std::getenv("PBH_GIBBS_LANES")) e->gibbs_lanes = std::atoi(gl);
   if (const char *ml = std::getenv("PBH_GMM_LANES")) e->gmm_lanes = std::atoi(ml);
+  if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
+  if (err == hipSuccess) {
+    std::vector<double> tab(pbh::kBm64Doubles);
+    pbh::bm64_tables(tab.data());
+    err = hipMalloc((void **)&e->bm64, tab.size() * sizeof(double));
+    if (err == hipSuccess)
+      err = hipMemcpy(e->bm64, tab.data(), tab.size() * sizeof(double),
+                      hipMemcpyHostToDevice);
+  }
   if (err != hipSuccess) {
-    delete e;
-    return fail(PBH_ERR_HIP, "stream/event creation failed: %s",
+    pbh_destroy(e);
+    return fail(PBH_ERR_HIP, "stream/event/table setup failed: %s",
                 hipGetErrorString(err));
   }
   *out = e;
@@ -211,6 +224,7 @@ int pbh_destroy(pbh_engine *e) {
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
+  dfree(e->bm64);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -542,7 +556,8 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
 int pbh_set_rng(pbh_engine *e, int32_t mode, uint64_t seed) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX &&
-      mode != PBH_RNG_PHILOX_F64 && mode != PBH_RNG_XOSHIRO)
+      mode != PBH_RNG_PHILOX_F64 && mode != PBH_RNG_XOSHIRO &&
+      mode != PBH_RNG_PHILOX_FP32)
     return fail(PBH_ERR_ARG, "bad rng mode %d", mode);
   e->rng = mode;
   e->seed = seed;
@@ -733,6 +748,8 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
                 "replay stream covers steps [%lld, %lld), run needs [%lld, %lld)",
                 (long long)e->rep_g0, (long long)(e->rep_g0 + e->rep_steps),
                 (long long)e->g, (long long)(e->g + n_steps));
+  if (e->rng == PBH_RNG_PHILOX_FP32 && e->has_gibbs)
+    return fail(PBH_ERR_UNSUPPORTED, "PHILOX_FP32 is a lane-pair MH comparison mode");
   if (e->cap > 0) {
     const int64_t recs = (e->g + n_steps) / e->thin - e->rec_base;
     if (recs > e->cap)
@@ -784,7 +801,9 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gmm_lanes = e->gmm_lanes;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
+  k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
+  k.bm64 = e->bm64;
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
                       k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
                          ? (size_t)k.tn * sizeof(double) : 0;
@@ -817,7 +836,23 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
 int pbh_sync(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->spin_sync) {
+    // poll the stream: returns within a microsecond or so of the last
+    // kernel's completion (a blocking wait sleeps on the completion signal)
+    hipError_t q;
+    while ((q = hipStreamQuery(e->stream)) == hipErrorNotReady) {
+    }
+    HIP_TRY(q);
+  } else {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  return PBH_OK;
+}
+
+int pbh_set_collect(pbh_engine *e, int32_t flags) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (flags & ~PBH_COLLECT_MOMENTS) return fail(PBH_ERR_ARG, "bad collect flags %d", flags);
+  e->collect = flags;
   return PBH_OK;
 }
 
@@ -898,6 +933,27 @@ int pbh_get_moments(pbh_engine *e, double *sum, double *sumsq, int64_t *n_acc,
   if (sumsq) HIP_TRY(hipMemcpy(sumsq, e->msq, dn * sizeof(double), hipMemcpyDeviceToHost));
   if (n_acc) HIP_TRY(hipMemcpy(n_acc, e->nacc, e->n * sizeof(int64_t), hipMemcpyDeviceToHost));
   if (n_steps) *n_steps = e->mom_steps;
+  return PBH_OK;
+}
+
+int pbh_trace_stats(pbh_engine *e, int64_t first, int64_t count, double *sum,
+                    double *sumsq, int64_t *n_acc) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  int64_t rec = 0;
+  pbh_trace_len(e, &rec);
+  if (first < 0 || count < 0 || first + count > rec)
+    return fail(PBH_ERR_ARG, "trace range [%lld, %lld) outside [0, %lld)",
+                (long long)first, (long long)(first + count), (long long)rec);
+  HIP_TRY(hipSetDevice(e->device));
+  const int64_t n = e->n, W = (n + 63) / 64;
+  HIP_TRY(pbh::launch_trace_stats(e->tx, e->tacc, n, e->d, W, first, count,
+                                  e->msum, e->msq, e->nacc, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->mom_steps = count;
+  const size_t dn = (size_t)e->d * n;
+  if (sum) HIP_TRY(hipMemcpy(sum, e->msum, dn * sizeof(double), hipMemcpyDeviceToHost));
+  if (sumsq) HIP_TRY(hipMemcpy(sumsq, e->msq, dn * sizeof(double), hipMemcpyDeviceToHost));
+  if (n_acc) HIP_TRY(hipMemcpy(n_acc, e->nacc, n * sizeof(int64_t), hipMemcpyDeviceToHost));
   return PBH_OK;
 }
 
@@ -1103,6 +1159,42 @@ int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
   if (err != hipSuccess)
     return fail(PBH_ERR_HIP, "pbh_bool_perm_freq: %s", hipGetErrorString(err));
   if (kernel_ms) *kernel_ms = total / reps;
+  return PBH_OK;
+}
+
+int pbh_check_normals64(int device, int64_t n, const uint32_t *words,
+                        double *fast, double *ref) {
+  if (check_ptr(words, "words") || check_ptr(fast, "fast") || check_ptr(ref, "ref"))
+    return PBH_ERR_ARG;
+  if (n <= 0) return fail(PBH_ERR_ARG, "n must be positive");
+  HIP_TRY(hipSetDevice(device));
+  std::vector<double> tab(pbh::kBm64Doubles);
+  pbh::bm64_tables(tab.data());
+  uint32_t *dw = nullptr;
+  double *df = nullptr, *dr = nullptr, *dt = nullptr;
+  int rc = dalloc(dw, 4 * n);
+  if (!rc) rc = dalloc(df, 2 * n);
+  if (!rc) rc = dalloc(dr, 2 * n);
+  if (!rc) rc = dalloc(dt, tab.size());
+  hipError_t err = hipSuccess;
+  if (!rc) {
+    err = hipMemcpy(dw, words, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (err == hipSuccess)
+      err = hipMemcpy(dt, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = pbh::launch_check_normals64(n, dw, dt, df, dr);
+    if (err == hipSuccess) err = hipMemcpy(fast, df, 2 * n * sizeof(double), hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(ref, dr, 2 * n * sizeof(double), hipMemcpyDeviceToHost);
+  }
+  dfree(dw); dfree(df); dfree(dr); dfree(dt);
+  if (rc) return rc;
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_check_normals64: %s", hipGetErrorString(err));
+  return PBH_OK;
+}
+
+int pbh_bm64_tables(double *out) {
+  if (check_ptr(out, "out")) return PBH_ERR_ARG;
+  pbh::bm64_tables(out);
   return PBH_OK;
 }
 

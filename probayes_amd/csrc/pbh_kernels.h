@@ -76,8 +76,11 @@ struct KArgs {
   int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
   int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
   // ---- moments ----
+  int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;
   int64_t *nacc;
+  // ---- production fp64 normals: bm64 tables (pbh_device.h), global copy
+  const double *bm64;
 };
 
 // The production Gibbs kernel runs for the Philox RNG without debug records,
@@ -94,6 +97,16 @@ hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
 bool mh_dim_supported(int d);
 hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
                                 double *ref);
+// bm64_pair (the production fp64 normals) and its libm form on n blocks.
+hipError_t launch_check_normals64(int64_t n, const uint32_t *words,
+                                  const double *tab, double *fast, double *ref);
+// per-chain sums / sums of squares / accept counts of trace records
+hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
+                              int32_t d, int64_t W, int64_t first,
+                              int64_t count, double *sum, double *sumsq,
+                              int64_t *nacc, hipStream_t s);
+// Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
+void bm64_tables(double *out);
 // Legacy (NumPy RandomState) stream generation (pbh_legacy.hip).
 struct LegacyArgs {
   uint32_t *key;        // MT19937 words [624][n]

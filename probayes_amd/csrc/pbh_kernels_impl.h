@@ -359,11 +359,16 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   // FAST = production Philox path (fp32 normals, FMA-corrected divisions);
   // REPLAY and PHILOX_F64 keep the reference's arithmetic exactly.
   constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
+  // production Gaussian deltas draw bm64 fp64 normals from LDS tables
+  constexpr bool TAB = FAST && (PROP == 0 || PROP == PBH_PROP_GAUSS);
   const int prop = PROP ? PROP : a.prop;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
+  const bool mom = a.moments != 0;
   // production modes with the symmetric ratio form: the acceptance filter
   const bool simple = FAST && a.simple_acc && !a.debug;
   extern __shared__ double s_obs[];
+  __shared__ double s_bmt[TAB ? kBm64Doubles : 2];
+  if constexpr (TAB) bm64_load(s_bmt, a.bm64);
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool active = c < a.n;
   const int64_t cc = active ? c : 0;
@@ -413,10 +418,11 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       if (prop == PBH_PROP_GAUSS) {
 #pragma unroll
         for (int p = 0; p < (D + 1) / 2; ++p) {
-          const uint32_t wu = xo_next(xs);
-          const uint32_t wa = xo_next(xs);
-          double z1;
-          r[2 * p] = fast_normal_pair(wu, wa, z1);
+          const uint32_t w0 = xo_next(xs), w1 = xo_next(xs);
+          const uint32_t w2 = xo_next(xs), w3 = xo_next(xs);
+          double z0, z1;
+          bm64_pair(w0, w1, w2, w3, s_bmt, z0, z1);
+          r[2 * p] = z0;
           if (2 * p + 1 < D) r[2 * p + 1] = z1;
         }
       } else {
@@ -429,34 +435,24 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       tw0 = xo_next(xs);
       tw1 = xo_next(xs);
       thr = u01(tw0, tw1);
-    } else if (FAST && prop == PBH_PROP_GAUSS) {
-      // two normal pairs per Philox block; an odd pair count leaves the
-      // block's second half for the 53-bit threshold
-      constexpr int P = (D + 1) / 2;
+    } else if (TAB && prop == PBH_PROP_GAUSS) {
+      // one bm64 fp64 normal pair per Philox block; t's leading 14 bits are
+      // block 0's spare bits, the rest come from block 0x40 -- the same t
+      // as the multi-lane GMM kernel's (its lead + fallback block)
+      uint32_t lead = 0;
 #pragma unroll
-      for (int q = 0; q < (P + 1) / 2; ++q) {
-        const u32x4 w = philox4x32_10(ctr(q, g, chain), a.seed_lo, a.seed_hi);
-        double z1;
-        const double z0 = fast_normal_pair(w.x, w.z, z1);
-        if (4 * q < D) r[4 * q] = z0;
-        if (4 * q + 1 < D) r[4 * q + 1] = z1;
-        if (2 * q + 1 < P) {
-          double z3;
-          const double z2 = fast_normal_pair(w.y, w.w, z3);
-          if (4 * q + 2 < D) r[4 * q + 2] = z2;
-          if (4 * q + 3 < D) r[4 * q + 3] = z3;
-        } else {
-          tw0 = w.y;
-          tw1 = w.w;
-          thr = u01(w.y, w.w);
-        }
+      for (int p = 0; p < (D + 1) / 2; ++p) {
+        const u32x4 w = philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi);
+        double z0, z1;
+        bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
+        r[2 * p] = z0;
+        if (2 * p + 1 < D) r[2 * p + 1] = z1;
+        if (p == 0) lead = bm64_spare(w.x, w.z);
       }
-      if (P % 2 == 0) {
-        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
-        tw0 = w.x;
-        tw1 = w.y;
-        thr = u01(w.x, w.y);
-      }
+      const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+      tw0 = (lead << 18) | (w.x >> 14);
+      tw1 = w.y;
+      thr = u01(tw0, tw1);
     } else {
       if (prop == PBH_PROP_GAUSS) {
 #pragma unroll
@@ -544,11 +540,13 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       lp = lpp;
       eB = eA;
     }
-    nacc += acc ? 1 : 0;
+    if (mom) {   // wave-uniform
+      nacc += acc ? 1 : 0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      ms[k] += x[k];
-      mq[k] += x[k] * x[k];
+      for (int k = 0; k < D; ++k) {
+        ms[k] += x[k];
+        mq[k] += x[k] * x[k];
+      }
     }
     // ---- trace (every thin-th step, wave-uniform condition) ----
     const bool rec_now = ph == 0;
@@ -577,13 +575,16 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 
   if (active) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      a.x[k * a.n + c] = x[k];
-      a.msum[k * a.n + c] += ms[k];
-      a.msq[k * a.n + c] += mq[k];
-    }
+    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
     a.lp[c] = lp;
-    a.nacc[c] += nacc;
+    if (mom) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        a.msum[k * a.n + c] += ms[k];
+        a.msq[k * a.n + c] += mq[k];
+      }
+      a.nacc[c] += nacc;
+    }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
   }
 }
@@ -695,51 +696,87 @@ __device__ __forceinline__ double part_max(double v) {
 
 
 
-// Production draws of a PAIR of half-steps (steps 2P, 2P + 1) of one lane:
-// NP = H / 2 Box-Muller pairs per step from NP Philox blocks (q < NP), and
-// one more block q = NP holding the odd normal of each step (H odd; its
-// spare bits carry the step's 14-bit threshold lead) or the two threshold
-// leads (H even, 24 bits).  3 blocks per 2 steps at H = 5 instead of 4, and
-// 2.5 Box-Muller evaluations per step instead of 3.
-template <int H>
-__device__ __forceinline__ void pair2_draw_philox(const KArgs &a, int h,
-                                                  int64_t P, int64_t chain,
-                                                  double (&ra)[H], double (&rb)[H],
-                                                  uint32_t &ta, uint32_t &tb) {
-  constexpr int NP = H / 2;
+// Production draws of a PAIR of steps (2P, 2P + 1) for one lane half: H
+// normals per step.  PHILOX: H Philox blocks q < H (counter q + 16 h), one
+// bm64 fp64 Box-Muller pair each -- normals 0..H-1 feed step A, H..2H-1
+// step B -- and the steps' threshold leads from the blocks' spare bits
+// (LB = 24 bits from two blocks at H >= 4, else 14 from one).  PHILOX_FP32
+// (comparison mode): the round-1 fp32 draws, NP = H / 2 blocks of two fp32
+// pairs plus one block holding the odd normals and 14-bit leads.
+template <int H, int RNG>
+struct PairDraw {
+  static constexpr bool F32 = RNG == PBH_RNG_PHILOX_FP32;
+  static constexpr int LB = F32 ? ((H % 2 == 1) ? 14 : 24) : (H >= 4 ? 24 : 14);
+
+  __device__ __forceinline__ static void draw(const KArgs &a, const double *bmt,
+                                              int h, int64_t P, int64_t chain,
+                                              double (&ra)[H], double (&rb)[H],
+                                              uint32_t &ta, uint32_t &tb) {
+    if constexpr (F32) {
+      constexpr int NP = H / 2;
 #pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const u32x4 w = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
-    double z0, z1, z2, z3;
-    z0 = fast_normal_pair(w.x, w.z, z1);
-    z2 = fast_normal_pair(w.y, w.w, z3);
-    // global pairs 2q, 2q + 1 of the step pair: 0..NP-1 -> step A, NP.. -> B
+      for (int q = 0; q < NP; ++q) {
+        const u32x4 w = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+        double z0, z1, z2, z3;
+        z0 = fast_normal_pair(w.x, w.z, z1);
+        z2 = fast_normal_pair(w.y, w.w, z3);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int gp = 2 * q + e;
-      const double u = e ? z2 : z0, v = e ? z3 : z1;
-      if (gp < NP) { ra[2 * gp] = u; ra[2 * gp + 1] = v; }
-      else { rb[2 * (gp - NP)] = u; rb[2 * (gp - NP) + 1] = v; }
+        for (int e = 0; e < 2; ++e) {
+          const int gp = 2 * q + e;
+          const double u = e ? z2 : z0, v = e ? z3 : z1;
+          if (gp < NP) { ra[2 * gp] = u; ra[2 * gp + 1] = v; }
+          else { rb[2 * (gp - NP)] = u; rb[2 * (gp - NP) + 1] = v; }
+        }
+      }
+      const u32x4 w = philox4x32_10(ctr(NP + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+      if constexpr (H % 2 == 1) {
+        ra[H - 1] = fast_normal_single(w.x, w.y, ta);
+        rb[H - 1] = fast_normal_single(w.z, w.w, tb);
+      } else {
+        ta = w.x >> 8;
+        tb = w.y >> 8;
+      }
+    } else {
+      uint32_t sp[H];
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const u32x4 w = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+        double z0, z1;
+        bm64_pair(w.x, w.y, w.z, w.w, bmt, z0, z1);
+        sp[q] = bm64_spare(w.x, w.z);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int n = 2 * q + e;
+          const double z = e ? z1 : z0;
+          if (n < H) ra[n] = z;
+          else rb[n - H] = z;
+        }
+      }
+      if constexpr (H >= 4) {
+        ta = (sp[0] << 10) | (sp[1] >> 4);
+        tb = (sp[H - 2] << 10) | (sp[H - 1] >> 4);
+      } else {
+        ta = sp[0];
+        tb = sp[H - 1];
+      }
     }
   }
-  const u32x4 w = philox4x32_10(ctr(NP + 16 * h, P, chain), a.seed_lo, a.seed_hi);
-  if constexpr (H % 2 == 1) {
-    ra[H - 1] = fast_normal_single(w.x, w.y, ta);
-    rb[H - 1] = fast_normal_single(w.z, w.w, tb);
-  } else {
-    ta = w.x >> 8;
-    tb = w.y >> 8;
-  }
-}
+};
 
-template <int D, int RNG>
-__global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
+template <int D, int RNG, bool MOM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void mh_pair_kernel(KArgs a) {
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
   constexpr int H = D / 2;
-  constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
+  constexpr bool PHX = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_PHILOX_FP32;
+  constexpr bool FAST = PHX || RNG == PBH_RNG_XOSHIRO;
   constexpr bool REPLAY = RNG == PBH_RNG_REPLAY;
-  constexpr int LB = (H % 2 == 1) ? 14 : 24;   // Philox threshold lead bits
+  constexpr bool TAB = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
+  using PD = PairDraw<H, RNG>;
+  __shared__ double s_bmt[TAB ? kBm64Doubles : 2];
+  if constexpr (TAB) bm64_load(s_bmt, a.bm64);
   const bool lin = a.pscale == PBH_PSCALE_LIN;
+  constexpr bool mom = MOM;   // running moments compiled in or out
   const int lane = threadIdx.x & 63;
   const bool hi = lane >= 32;
   const int h = hi ? 1 : 0;
@@ -749,6 +786,10 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   const int64_t cc = active ? c : 0;
   const int k0 = h * H;   // first dim of this half
   const uint64_t act_mask = __ballot(active);
+  // byte offsets of this lane's trace elements inside a record (< 4 GB)
+  const uint32_t boff = (uint32_t)(((int64_t)k0 * a.n + cc) * 8);
+  const uint32_t bstride = (uint32_t)(a.n * 8);
+  const uint32_t loff = (uint32_t)(cc * 8);
 
   // Per-lane model constants in VGPRs for the whole launch (the half's dims
   // differ between lanes, so these are vector values, loaded once).
@@ -789,9 +830,12 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
   // record (g + 1) / thin - 1 - rec_base.
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  // Drain the entry loads here: a wait for them inside the loop would also
+  // wait for every trace store issued before it.
+  __builtin_amdgcn_s_waitcnt(0);
 
-  // One chain-step.  (r, t0, t1) are this step's draws (production Philox:
-  // supplied by the caller, t0 = the LB-bit threshold lead).
+  // One chain-step.  (r, t0, t1) are this step's draws (Philox: supplied by
+  // the caller, t0 = the LB-bit threshold lead).
   auto step = [&](int s, double (&r)[H], uint32_t &t0, uint32_t &t1) {
     const int64_t g = a.g0 + s;
     double thr = 0.;
@@ -801,21 +845,22 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
       thr = row[(int64_t)D * a.n];   // used by half 1
     } else if (RNG == PBH_RNG_XOSHIRO) {
-      // this half's stream: two words per normal pair, then the threshold
-      // (drawn by both halves so each stream advances the same per step)
+      // this half's stream: four words per fp64 normal pair, then the
+      // threshold (drawn by both halves so each stream advances the same)
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
-        const uint32_t wu = xo_next(xs);
-        const uint32_t wa = xo_next(xs);
-        double z1;
-        r[2 * p] = fast_normal_pair(wu, wa, z1);
+        const uint32_t w0 = xo_next(xs), w1 = xo_next(xs);
+        const uint32_t w2 = xo_next(xs), w3 = xo_next(xs);
+        double z0, z1;
+        bm64_pair(w0, w1, w2, w3, s_bmt, z0, z1);
+        r[2 * p] = z0;
         if (2 * p + 1 < H) r[2 * p + 1] = z1;
       }
       t0 = xo_next(xs);
       t1 = xo_next(xs);
-    } else if (RNG == PBH_RNG_PHILOX) {
-      // drawn by the caller, a step pair ahead (pair2_draw_philox)
-    } else {   // PHILOX_F64: fp64 Box-Muller
+    } else if (PHX) {
+      // drawn by the caller, a step pair ahead (PairDraw)
+    } else {   // PHILOX_F64: libm fp64 Box-Muller
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
         double z0, z1;
@@ -844,8 +889,9 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
         if (i & 1) p1 = __builtin_fma(u, u, p1);
         else p0 = __builtin_fma(u, u, p0);
       }
-      const double part = p0 + p1;
-      lpp = -((part + swap_f64(part, hi)) + a.ksum);
+      double lo, up;
+      halves_f64(p0 + p1, lo, up);   // the two halves' sums, in every lane
+      lpp = -((lo + up) + a.ksum);
     } else {
       double tm[H];
 #pragma unroll
@@ -869,19 +915,18 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
       q = q < 1. ? q : 1.;
       acc = first || q >= thr;
     } else {
-      const Decision dc = RNG == PBH_RNG_PHILOX
-                              ? accept_filter_lead<LB>(lpp, lp, t0, lin)
+      const Decision dc = PHX ? accept_filter_lead<PD::LB>(lpp, lp, t0, lin)
                               : accept_filter(lpp, lp, t0, lin);
       acc = first || dc.acc;
       const bool need = hi && !first && dc.need;
       if (__ballot(need)) {   // wave-uniform, rare
         if (need) {
           double t;
-          if (RNG == PBH_RNG_PHILOX) {
+          if (PHX) {
             // t's remaining 53 - LB bits from a block of this step alone
             const u32x4 w = philox4x32_10(ctr(0x40u + 16u * h, g, chain),
                                           a.seed_lo, a.seed_hi);
-            t = u01((t0 << (32 - LB)) | (w.x >> LB), w.y);
+            t = u01((t0 << (32 - PD::LB)) | (w.x >> PD::LB), w.y);
           } else {
             t = u01(t0, t1);
           }
@@ -897,22 +942,24 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     for (int i = 0; i < H; ++i) x[i] = accl ? xp[i] : x[i];
     if (REPLAY) eB = accl ? eA : eB;
     lp = accl ? lpp : lp;
-    nacc += accl ? 1 : 0;
+    if constexpr (mom) {
+      nacc += accl ? 1 : 0;
 #pragma unroll
-    for (int i = 0; i < H; ++i) {
-      ms[i] += x[i];
-      mq[i] = __builtin_fma(x[i], x[i], mq[i]);
+      for (int i = 0; i < H; ++i) {
+        ms[i] += x[i];
+        mq[i] = __builtin_fma(x[i], x[i], mq[i]);
+      }
     }
     const bool rec_now = ph == 0;
     const int64_t rec = ri;
     ph = (ph + 1 == a.thin) ? 0 : ph + 1;   // next step's phase
     ri += (ph == 0) ? 1 : 0;
     if (rec_now && rec >= 0 && rec < a.rec_cap) {
-      double *row = a.tx + rec * D * a.n;
+      double *row = a.tx + rec * D * a.n;   // wave-uniform
       if (active) {
 #pragma unroll
-        for (int i = 0; i < H; ++i) __builtin_nontemporal_store(x[i], &row[(k0 + i) * a.n + c]);
-        if (hi) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
+        for (int i = 0; i < H; ++i) st_buf(row, boff, i * bstride, x[i]);
+        if (hi) st_buf(a.tlp + rec * a.n, loff, 0, lp);
       }
       // 32 chains per wave: the upper half's ballot bits are the mask word
       if (lane == 32 && (c >> 5) < 2 * a.W)
@@ -921,37 +968,58 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
     }
   };
 
-  if constexpr (RNG == PBH_RNG_PHILOX) {
+  if constexpr (PHX) {
     // Draws come per step PAIR (2P, 2P + 1), P = absolute step / 2, so a run
-    // split into launches at any step sees the same stream.  The next pair's
-    // blocks are issued while the current pair's fp64 chain runs (the draws
-    // never depend on state): ping-pong over two draw sets.
-    double cA[H], cB[H], nA[H], nB[H];
-    uint32_t ctA = 0, ctB = 0, ntA = 0, ntB = 0, t1 = 0;
+    // split into launches at any step sees the same stream.  PHILOX_FP32
+    // issues the next pair's blocks while the current pair's fp64 chain runs
+    // (ping-pong over two draw sets); the fp64 normals hold too many live
+    // registers for that at two waves per SIMD, so PHILOX draws each pair
+    // just before its two steps and relies on the SIMD's other wave.
+    double cA[H], cB[H];
+    uint32_t ctA = 0, ctB = 0, t1 = 0;
     int s = 0;
-    pair2_draw_philox<H>(a, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
-    if ((a.g0 & 1) && s < a.n_steps) {   // launch starts on a pair's 2nd step
-      step(s, cB, ctB, t1);
-      ++s;
-      if (s < a.n_steps)
-        pair2_draw_philox<H>(a, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+    if constexpr (PD::F32) {
+      double nA[H], nB[H];
+      uint32_t ntA = 0, ntB = 0;
+      PD::draw(a, s_bmt, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
+      if ((a.g0 & 1) && s < a.n_steps) {   // launch starts on a pair's 2nd step
+        step(s, cB, ctB, t1);
+        ++s;
+        if (s < a.n_steps)
+          PD::draw(a, s_bmt, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+      }
+      for (; s + 3 < a.n_steps; s += 4) {
+        PD::draw(a, s_bmt, h, ((a.g0 + s) >> 1) + 1, chain, nA, nB, ntA, ntB);
+        step(s, cA, ctA, t1);
+        step(s + 1, cB, ctB, t1);
+        PD::draw(a, s_bmt, h, ((a.g0 + s) >> 1) + 2, chain, cA, cB, ctA, ctB);
+        step(s + 2, nA, ntA, t1);
+        step(s + 3, nB, ntB, t1);
+      }
+      if (s + 1 < a.n_steps) {
+        step(s, cA, ctA, t1);
+        step(s + 1, cB, ctB, t1);
+        s += 2;
+        if (s < a.n_steps)
+          PD::draw(a, s_bmt, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+      }
+      if (s < a.n_steps) step(s, cA, ctA, t1);
+    } else {
+      if (a.g0 & 1) {   // launch starts on a pair's 2nd step
+        PD::draw(a, s_bmt, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
+        step(s, cB, ctB, t1);
+        ++s;
+      }
+      for (; s + 1 < a.n_steps; s += 2) {
+        PD::draw(a, s_bmt, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+        step(s, cA, ctA, t1);
+        step(s + 1, cB, ctB, t1);
+      }
+      if (s < a.n_steps) {
+        PD::draw(a, s_bmt, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
+        step(s, cA, ctA, t1);
+      }
     }
-    for (; s + 3 < a.n_steps; s += 4) {
-      pair2_draw_philox<H>(a, h, ((a.g0 + s) >> 1) + 1, chain, nA, nB, ntA, ntB);
-      step(s, cA, ctA, t1);
-      step(s + 1, cB, ctB, t1);
-      pair2_draw_philox<H>(a, h, ((a.g0 + s) >> 1) + 2, chain, cA, cB, ctA, ctB);
-      step(s + 2, nA, ntA, t1);
-      step(s + 3, nB, ntB, t1);
-    }
-    if (s + 1 < a.n_steps) {
-      step(s, cA, ctA, t1);
-      step(s + 1, cB, ctB, t1);
-      s += 2;
-      if (s < a.n_steps)
-        pair2_draw_philox<H>(a, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
-    }
-    if (s < a.n_steps) step(s, cA, ctA, t1);
   } else {
     double r[H];
     uint32_t t0 = 0, t1 = 0;
@@ -960,36 +1028,95 @@ __global__ __launch_bounds__(kBlock) void mh_pair_kernel(KArgs a) {
 
   if (active) {
 #pragma unroll
-    for (int i = 0; i < H; ++i) {
-      a.x[(k0 + i) * a.n + c] = x[i];
-      a.msum[(k0 + i) * a.n + c] += ms[i];
-      a.msq[(k0 + i) * a.n + c] += mq[i];
-    }
-    if (hi) {
-      a.lp[c] = lp;
-      a.nacc[c] += nacc;
+    for (int i = 0; i < H; ++i) a.x[(k0 + i) * a.n + c] = x[i];
+    if (hi) a.lp[c] = lp;
+    if constexpr (mom) {
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        a.msum[(k0 + i) * a.n + c] += ms[i];
+        a.msq[(k0 + i) * a.n + c] += mq[i];
+      }
+      if (hi) a.nacc[c] += nacc;
     }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, h, c, xs);
   }
 }
-
 // ---------------------------------------------------------------------------
 // Multi-lane MH kernel for the Gaussian-mixture target with the callable
-// Gaussian delta (cfg5, production RNG).  At d = 2 the one-chain-per-lane
-// kernel leaves every other SIMD idle at 32 768 chains; here one chain is a
-// group of L lanes (rows of 64 / L lanes).  Every lane of a group holds the
-// whole state and draws the same proposal (the same Philox block); the K
-// components are dealt over the parts (k = p + L kk), each part forms its
-// partial log-sum-exp (m_p, s_p), and the group combines them:
-// lse = M + log(sum_p s_p exp(m_p - M)), M = max_p m_p.  Acceptance is the
-// filtered ratio form, identical in every lane of the group.
+// Gaussian delta (cfg5, production RNG).  At d = 2 a chain per lane leaves
+// SIMDs idle at 32 768 chains; here one chain is a group of L lanes (rows of
+// 64 / L lanes) holding the whole state.
+//  * Draws: steps come in aligned groups of L (absolute step / L), and part
+//    p of a group draws step L G + p alone (bm64 fp64 normals + a 14-bit
+//    threshold lead from the block's spare bits); one all-gather over the
+//    group's lanes (v_permlane16/32_swap) hands every lane the L steps'
+//    draws, so each lane runs 1/L of the Philox and Box-Muller work.
+//  * Density: the K components are dealt over the parts (k = p + L kk);
+//    each part forms its partial log-sum-exp and the group combines them,
+//    lse = M + log S, S = sum_p sum_k exp(v_k - M), M = max_k v_k.
+//  * Acceptance never waits for that log: the state's density is carried as
+//    (M, S) besides lp = M + log S, and the filter's ratio is
+//    exp(M' - M) S' / S -- the log of S' (the recorded v.prob) runs off the
+//    step-to-step dependency chain.  Undecided steps (about 1e-4) evaluate the
+//    exact ratio form of (lp', lp) under a wave-uniform branch, as everywhere.
 // ---------------------------------------------------------------------------
+template <int L>
+__device__ __forceinline__ void gather_f64(double v, double (&all)[L]) {
+  if constexpr (L == 2) {
+    halves_f64(v, all[0], all[1]);
+  } else {
+    static_assert(L == 4, "lanes per chain: 2 or 4");
+    double ev, od;
+    rowpair_f64(v, ev, od);
+    halves_f64(ev, all[0], all[2]);
+    halves_f64(od, all[1], all[3]);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void gather_u32(uint32_t v, uint32_t (&all)[L]) {
+  if constexpr (L == 2) {
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    all[0] = a[0];
+    all[1] = a[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const auto e = __builtin_amdgcn_permlane32_swap(r[0], r[0], false, false);
+    const auto o = __builtin_amdgcn_permlane32_swap(r[1], r[1], false, false);
+    all[0] = e[0];
+    all[2] = e[1];
+    all[1] = o[0];
+    all[3] = o[1];
+  }
+}
+
+// filter of the ratio form for a state carried as (M, S): e = exp(M' - M)
+// S' / S in fp32 (within 3e-6 of the ratio wherever |M|, |M'| <= 698, K <= 7)
+template <int LB>
+__device__ __forceinline__ Decision accept_filter_ms(double Mp, double Sp,
+                                                     double M, double S,
+                                                     uint32_t lead) {
+  constexpr float w = 1.0f / (float)(1u << LB);
+  const float e = __builtin_amdgcn_exp2f((float)((Mp - M) * 1.4426950408889634)) *
+                  (float)(Sp / S);
+  const float tlo = (float)lead * w;
+  const float thi = tlo + w;
+  const bool inr = __builtin_fabs(Mp) <= 698. && __builtin_fabs(M) <= 698.;
+  const bool af = thi <= e * 0.999996f;
+  const bool rf = tlo > e * 1.000004f;
+  return Decision{inr && af, !(inr && (af || rf))};
+}
+
 template <int D, int K, int L>
 __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
   constexpr int KL = (K + L - 1) / L;    // component slots per part
   constexpr int CW = 64 / L;             // chains per wavefront
+  constexpr int P = (D + 1) / 2;         // bm64 blocks per step
+  constexpr int LB = 14;                 // threshold lead bits (spare bits)
   constexpr double kNegInf = -__builtin_inf();
-  const bool lin = a.pscale == PBH_PSCALE_LIN;
+  __shared__ double s_bmt[kBm64Doubles];
+  bm64_load(s_bmt, a.bm64);
+  const bool mom = a.moments != 0;
   const int lane = threadIdx.x & 63;
   const int p = lane / CW;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
@@ -1012,6 +1139,12 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
 #pragma unroll
     for (int i = 0; i < D; ++i) cmu[kk][i] = ok ? a.tb[k * D + i] : 0.;
   }
+  double psc[D], plc[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    psc[i] = cld(a.pscl, i);
+    plc[i] = cld(a.ploc, i);
+  }
   double x[D], ms[D], mq[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
@@ -1020,105 +1153,123 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
     mq[i] = 0.;
   }
   double lp = a.lp[cc];
+  double lm = lp, ls = 1.0;   // the state's density as (M, S): lp = M + log S
   int64_t nacc = 0;
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  const uint32_t boff = (uint32_t)(cc * 8), bstride = (uint32_t)(a.n * 8);
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
 
-  for (int s = 0; s < a.n_steps; ++s) {
-    const int64_t g = a.g0 + s;
-    // ---- draws: mh_kernel's production Gaussian path (same counters) ----
-    constexpr int P = (D + 1) / 2;
-    double r[D];
-    uint32_t tw0 = 0, tw1 = 0;
+  const int64_t gend = a.g0 + a.n_steps;
+  for (int64_t G = a.g0 / L; G * L < gend; ++G) {
+    // ---- this part's draws for step L G + p, then the group's all-gather
+    double rown[D];
+    uint32_t lown = 0;
 #pragma unroll
-    for (int q = 0; q < (P + 1) / 2; ++q) {
-      const u32x4 w = philox4x32_10(ctr(q, g, chain), a.seed_lo, a.seed_hi);
-      double z1;
-      const double z0 = fast_normal_pair(w.x, w.z, z1);
-      if (4 * q < D) r[4 * q] = z0;
-      if (4 * q + 1 < D) r[4 * q + 1] = z1;
-      if (2 * q + 1 < P) {
-        double z3;
-        const double z2 = fast_normal_pair(w.y, w.w, z3);
-        if (4 * q + 2 < D) r[4 * q + 2] = z2;
-        if (4 * q + 3 < D) r[4 * q + 3] = z3;
+    for (int q = 0; q < P; ++q) {
+      const u32x4 w = philox4x32_10(ctr(q, G * L + p, chain), a.seed_lo, a.seed_hi);
+      double z0, z1;
+      bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
+      rown[2 * q] = z0;
+      if (2 * q + 1 < D) rown[2 * q + 1] = z1;
+      if (q == 0) lown = bm64_spare(w.x, w.z);
+    }
+    double rall[D][L];
+    uint32_t lall[L];
+#pragma unroll
+    for (int i = 0; i < D; ++i) gather_f64<L>(rown[i], rall[i]);
+    gather_u32<L>(lown, lall);
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int64_t g = G * L + j;
+      if (g < a.g0 || g >= gend) continue;   // wave-uniform
+      const int s = (int)(g - a.g0);
+      double xp[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) xp[i] = x[i] + __builtin_fma(rall[i][j], psc[i], plc[i]);
+      // ---- partial log-sum-exp over this part's components, then the group's
+      double v[KL];
+#pragma unroll
+      for (int kk = 0; kk < KL; ++kk) {
+        double acc = c0[kk];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          const double u = (xp[i] - cmu[kk][i]) * cw[kk];
+          acc = __builtin_fma(-u, u, acc);
+        }
+        v[kk] = acc;
+      }
+      double m = v[0];
+#pragma unroll
+      for (int kk = 1; kk < KL; ++kk) m = __builtin_fmax(m, v[kk]);
+      const double M = part_max<L>(m);
+      double e = 0.;
+#pragma unroll
+      for (int kk = 0; kk < KL; ++kk) e += fast_exp(v[kk] - M);
+      const double S = part_sum<L>(any ? e : 0.);   // in [1, K]
+      // the recorded v.prob; the sum is in [1, K], the production log serves
+      const double lpp = M + fast_log(S);
+      // ---- acceptance (identical in every lane of the group) ----
+      bool acc;
+      if (!a.has_pred && s == 0) {
+        acc = true;                                  // s = None on step 1
+      } else if (a.acc_beta == 1.0) {
+        const Decision dc = accept_filter_ms<LB>(M, S, lm, ls, lall[j]);
+        acc = dc.acc;
+        if (__ballot(dc.need)) {   // wave-uniform, rare
+          if (dc.need) {
+            const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+            const double t = u01((lall[j] << (32 - LB)) | (w.x >> LB), w.y);
+            acc = ratio_accept(lpp, lp, t, false, a.log_npi);
+          }
+        }
       } else {
-        tw0 = w.y;
-        tw1 = w.w;
+        // e-tempered ratio form (App. A-1): the filter on (beta lp', beta lp)
+        const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
+        const Decision dc = accept_filter_lead<LB>(bA, bB, lall[j], false);
+        acc = dc.acc;
+        if (__ballot(dc.need)) {
+          if (dc.need) {
+            const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+            const double t = u01((lall[j] << (32 - LB)) | (w.x >> LB), w.y);
+            acc = ratio_accept(bA, bB, t, false, a.log_npi);
+          }
+        }
       }
-    }
-    if (P % 2 == 0) {
-      const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
-      tw0 = w.x;
-      tw1 = w.y;
-    }
-    double xp[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i)
-      xp[i] = x[i] + __builtin_fma(r[i], cld(a.pscl, i), cld(a.ploc, i));
-    // ---- partial log-sum-exp over this part's components, then the group's
-    double v[KL];
+      for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
+      lp = acc ? lpp : lp;
+      lm = acc ? M : lm;
+      ls = acc ? S : ls;
+      if (mom) {
+        nacc += acc ? 1 : 0;
 #pragma unroll
-    for (int kk = 0; kk < KL; ++kk) {
-      double acc = c0[kk];
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const double u = (xp[i] - cmu[kk][i]) * cw[kk];
-        acc = __builtin_fma(-u, u, acc);
+        for (int i = 0; i < D; ++i) {
+          if (i % L == p) {
+            ms[i] += x[i];
+            mq[i] = __builtin_fma(x[i], x[i], mq[i]);
+          }
+        }
       }
-      v[kk] = acc;
-    }
-    double m = v[0];
+      const bool rec_now = ph == 0;
+      const int64_t rec = ri;
+      ph = (ph + 1 == a.thin) ? 0 : ph + 1;
+      ri += (ph == 0) ? 1 : 0;
+      if (rec_now && rec >= 0 && rec < a.rec_cap) {
+        if (active) {
+          double *row = a.tx + rec * D * a.n;   // wave-uniform
 #pragma unroll
-    for (int kk = 1; kk < KL; ++kk) m = __builtin_fmax(m, v[kk]);
-    const double M = part_max<L>(m);
-    double e = 0.;
-#pragma unroll
-    for (int kk = 0; kk < KL; ++kk) e += fast_exp(v[kk] - M);
-    // the sum is in [1, K]: the production log (within 2 ulp) serves
-    const double lpp = M + fast_log(part_sum<L>(any ? e : 0.));
-    // ---- acceptance (identical in every lane of the group) ----
-    bool acc;
-    if (!a.has_pred && s == 0) {
-      acc = true;                                  // s = None on step 1
-    } else {
-      const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
-      const Decision dc = accept_filter(bA, bB, tw0, lin);
-      acc = dc.acc;
-      if (__ballot(dc.need)) {   // wave-uniform, rare
-        if (dc.need) acc = ratio_accept(bA, bB, u01(tw0, tw1), lin, a.log_npi);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
-    lp = acc ? lpp : lp;
-    nacc += acc ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      if (i % L == p) {
-        ms[i] += x[i];
-        mq[i] = __builtin_fma(x[i], x[i], mq[i]);
-      }
-    }
-    const bool rec_now = ph == 0;
-    const int64_t rec = ri;
-    ph = (ph + 1 == a.thin) ? 0 : ph + 1;
-    ri += (ph == 0) ? 1 : 0;
-    if (rec_now && rec >= 0 && rec < a.rec_cap) {
-      if (active) {
-        double *row = a.tx + rec * D * a.n;
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-          if (i % L == p) __builtin_nontemporal_store(x[i], &row[i * a.n + c]);
-        if (p == 0) __builtin_nontemporal_store(lp, &a.tlp[rec * a.n + c]);
-      }
-      // the parts agree: part 0's lanes (bits [0, CW)) carry the chains
-      const uint64_t am = __ballot(acc) & act_mask;
-      if (lane == 0 && wave < (64 / CW) * a.W) {   // stay inside the record
-        const int64_t wi = rec * (64 / CW) * a.W + wave;
-        if constexpr (CW == 32) reinterpret_cast<uint32_t *>(a.tacc)[wi] = (uint32_t)am;
-        else reinterpret_cast<uint16_t *>(a.tacc)[wi] = (uint16_t)am;
+          for (int i = 0; i < D; ++i)
+            if (i % L == p) st_buf(row, boff, i * bstride, x[i]);
+          if (p == (D % L)) st_buf(a.tlp + rec * a.n, boff, 0, lp);
+        }
+        // the parts agree: part 0's lanes (bits [0, CW)) carry the chains
+        const uint64_t am = __ballot(acc) & act_mask;
+        if (lane == 0 && wave < (64 / CW) * a.W) {   // stay inside the record
+          const int64_t wi = rec * (64 / CW) * a.W + wave;
+          if constexpr (CW == 32) reinterpret_cast<uint32_t *>(a.tacc)[wi] = (uint32_t)am;
+          else reinterpret_cast<uint16_t *>(a.tacc)[wi] = (uint16_t)am;
+        }
       }
     }
   }
@@ -1127,17 +1278,18 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
     for (int i = 0; i < D; ++i) {
       if (i % L == p) {
         a.x[i * a.n + c] = x[i];
-        a.msum[i * a.n + c] += ms[i];
-        a.msq[i * a.n + c] += mq[i];
+        if (mom) {
+          a.msum[i * a.n + c] += ms[i];
+          a.msq[i * a.n + c] += mq[i];
+        }
       }
     }
     if (p == 0) {
       a.lp[c] = lp;
-      a.nacc[c] += nacc;
+      if (mom) a.nacc[c] += nacc;
     }
   }
 }
-
 // ---------------------------------------------------------------------------
 // MFMA form of the mvn quadratic form for a wavefront of 64 chains:
 //   Y^T (16 x 16 chains) = U^T (16 x 4) . DEV^T (4 x 16 chains), K-chunks of 4
@@ -1267,10 +1419,12 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
       }
     }
     lp = MF ? mf.density(a, x, tile) : mvn_density<D>(a, x);
+    if (a.moments) {   // wave-uniform
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      ms[k] += x[k];
-      mq[k] += x[k] * x[k];
+      for (int k = 0; k < D; ++k) {
+        ms[k] += x[k];
+        mq[k] += x[k] * x[k];
+      }
     }
     const bool rec_now = ph == 0;
     const int64_t rec = ri;
@@ -1297,13 +1451,16 @@ __global__ __launch_bounds__(kBlock) void gibbs_kernel(KArgs a) {
   }
   if (active) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      a.x[k * a.n + c] = x[k];
-      a.msum[k * a.n + c] += ms[k];
-      a.msq[k * a.n + c] += mq[k];
-    }
+    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
     a.lp[c] = lp;
-    a.nacc[c] += a.n_steps;
+    if (a.moments) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        a.msum[k * a.n + c] += ms[k];
+        a.msq[k * a.n + c] += mq[k];
+      }
+      a.nacc[c] += a.n_steps;
+    }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
   }
 }
@@ -1504,10 +1661,12 @@ struct GibbsFastRun : GibbsFast<D, L> {
   // after a step: moments, trace record of x and u; returns the step's
   // record index, or -1 when the step is not recorded
   __device__ __forceinline__ int64_t post_x(const KArgs &a) {
+    if (a.moments) {   // wave-uniform
 #pragma unroll
-    for (int ii = 0; ii < M; ++ii) {
-      this->ms[ii] += this->xo[ii];
-      this->mq[ii] = __builtin_fma(this->xo[ii], this->xo[ii], this->mq[ii]);
+      for (int ii = 0; ii < M; ++ii) {
+        this->ms[ii] += this->xo[ii];
+        this->mq[ii] = __builtin_fma(this->xo[ii], this->xo[ii], this->mq[ii]);
+      }
     }
     const bool rec_now = ph == 0;
     const int64_t rec = ri;
@@ -1656,13 +1815,15 @@ void gibbs_fast_kernel(KArgs a) {
 #pragma unroll
     for (int ii = 0; ii < M; ++ii) {
       a.x[(p * M + ii) * a.n + c] = st.xo[ii];
-      a.msum[(p * M + ii) * a.n + c] += st.ms[ii];
-      a.msq[(p * M + ii) * a.n + c] += st.mq[ii];
+      if (a.moments) {
+        a.msum[(p * M + ii) * a.n + c] += st.ms[ii];
+        a.msq[(p * M + ii) * a.n + c] += st.mq[ii];
+      }
       a.gq[(p * M + ii) * a.n + c] = st.go[ii];
     }
     if (p == 0) {
       a.lp[c] = st.lp;
-      a.nacc[c] += a.n_steps;
+      if (a.moments) a.nacc[c] += a.n_steps;
       a.gq[D * a.n + c] = st.Q;
     }
   }
@@ -1687,18 +1848,26 @@ void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
                        block, lds, st, a);
 }
 
+template <int D, bool MOM>
+void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
+  if (a.rng == PBH_RNG_REPLAY)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_REPLAY, MOM>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_PHILOX)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX, MOM>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_XOSHIRO)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_XOSHIRO, MOM>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_PHILOX_FP32)
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_FP32, MOM>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_F64, MOM>), grid, block, 0, st, a);
+}
+
 template <int D>
 void launch_mh_pair(const KArgs &a, hipStream_t st) {
   const int64_t waves = (a.n + 31) / 32;
   const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
-  if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_REPLAY>), grid, block, 0, st, a);
-  else if (a.rng == PBH_RNG_PHILOX)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX>), grid, block, 0, st, a);
-  else if (a.rng == PBH_RNG_XOSHIRO)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_XOSHIRO>), grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_F64>), grid, block, 0, st, a);
+  if (a.moments) launch_mh_pair_m<D, true>(a, st, grid, block);
+  else launch_mh_pair_m<D, false>(a, st, grid, block);
 }
 
 // The lane-pair kernel covers the cfg2 form: diagonal Gaussian, callable
@@ -1706,6 +1875,7 @@ void launch_mh_pair(const KArgs &a, hipStream_t st) {
 inline bool pair_form(const KArgs &a) {
   return a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS &&
          a.ufun == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
+         a.d * a.n * 8 < (int64_t(1) << 32) &&   // 32-bit trace byte offsets
          (a.scores == PBH_SCORES_METROPOLIS ||
           (a.scores == PBH_SCORES_HASTINGS && a.tran_sym &&
            a.tran_kind == PBH_TRAN_CONST));
@@ -1715,7 +1885,8 @@ inline bool pair_form(const KArgs &a) {
 // ufun / prior / debug records.
 inline bool gmm_pair_form(const KArgs &a) {
   return a.rng == PBH_RNG_PHILOX && a.simple_acc && a.pair_ok && a.ufun == 0 &&
-         !a.has_prior && !a.debug && !a.has_tfun;
+         !a.has_prior && !a.debug && !a.has_tfun &&
+         a.d * a.n * 8 < (int64_t(1) << 32);   // 32-bit trace byte offsets
 }
 
 template <int D>
@@ -1726,6 +1897,7 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
       return hipGetLastError();
     }
   }
+  if (a.rng == PBH_RNG_PHILOX_FP32) return hipErrorInvalidValue;   // pair kernel only
   // Specialised forms: the cfg2 diagonal Gaussian with the callable Gaussian
   // delta at every d; the other example forms at the small d they use.
   if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS) {

@@ -238,6 +238,12 @@ class Engine:
   def sync(self):
     _lib.call('pbh_sync', self._h)
 
+  def set_collect(self, moments=True):
+    """moments=False: the kernels keep no running moments (no per-launch
+    read-modify-write); trace_stats() reduces the recorded trace instead."""
+    _lib.call('pbh_set_collect', self._h,
+              _lib.COLLECT_MOMENTS if moments else 0)
+
   def last_run_ms(self):
     ms, nl = _c.c_double(), _c.c_int64()
     _lib.call('pbh_last_run_ms', self._h, _c.byref(ms), _c.byref(nl))
@@ -291,6 +297,20 @@ class Engine:
               na.ctypes.data_as(_c.POINTER(_c.c_int64)), _c.byref(steps))
     return {'sum': s.T.copy(), 'sumsq': q.T.copy(), 'n_acc': na,
             'n_steps': steps.value}
+
+  def trace_stats(self, first=0, count=None):
+    """Per-chain sum / sumsq / n_acc of trace records [first, first +
+    count), reduced on the device (also replaces the engine's moments)."""
+    count = self.trace_len() - first if count is None else count
+    n, d = self.n, self.dim
+    s = np.empty((d, n))
+    q = np.empty((d, n))
+    na = np.empty(n, np.int64)
+    _lib.call('pbh_trace_stats', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(count)), _dp(s), _dp(q),
+              na.ctypes.data_as(_c.POINTER(_c.c_int64)))
+    return {'sum': s.T.copy(), 'sumsq': q.T.copy(), 'n_acc': na,
+            'n_steps': int(count)}
 
   def reset_moments(self):
     _lib.call('pbh_reset_moments', self._h)

@@ -46,3 +46,81 @@ def test_fast_box_muller_matches_libm_and_numpy():
   # NumPy rounds the angle 2 pi u2 before cos/sin: absolute error ~ r ulp
   assert np.max(np.abs(fast - host) / np.maximum(1.0, r)[:, None]) < 1e-14
   assert np.isfinite(fast).all()
+
+
+def _normals64(words):
+  words = np.ascontiguousarray(words, np.uint32)
+  n = words.shape[0]
+  fast = np.empty((n, 2))
+  ref = np.empty((n, 2))
+  _lib.call('pbh_check_normals64', 0, n, words.ctypes.data_as(_lib._u32p),
+            fast.ctypes.data_as(_lib._dp), ref.ctypes.data_as(_lib._dp))
+  return fast, ref
+
+
+def _bm64_host(w):
+  """bm64_pair's construction in NumPy (pbh_device.h): u1 = (k1 + 1/2)
+  2^-52 from x[19:0]:y, the quarter-turn angle from z[29:22] and z[19:0]:w,
+  signs z[31], z[30]."""
+  w = w.astype(np.uint64)
+  k1 = ((w[:, 0] & 0xFFFFF) << 32) | w[:, 1]
+  u1 = (k1.astype(np.float64) + 0.5) * 2.0 ** -52
+  k2 = ((w[:, 2] & 0xFFFFF) << 32) | w[:, 3]
+  j = ((w[:, 2] >> 22) & 0xFF).astype(np.float64)
+  ang = (j + k2.astype(np.float64) * 2.0 ** -52) * (np.pi / 2 / 256)
+  r = np.sqrt(-2.0 * np.log(u1))
+  s0 = np.where((w[:, 2] >> 31) & 1, -1.0, 1.0)
+  s1 = np.where((w[:, 2] >> 30) & 1, -1.0, 1.0)
+  return np.stack([s0 * r * np.cos(ang), s1 * r * np.sin(ang)], 1), r
+
+
+def test_bm64_normals_match_libm_and_numpy():
+  """The production fp64 normals (bm64_pair: 1025-entry log table + degree-5
+  log1p, rsq + Newton sqrt, 256-entry quarter-turn sin/cos table) against the
+  same construction through ocml's libm and through NumPy on the host:
+  within a few ulp (absolute below |z| = 1, relative above)."""
+  rng = np.random.RandomState(11)
+  n = 1 << 20
+  w = rng.randint(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+  # extremes: u1 at 2^-53 (largest r) and 1 - 2^-53 (r -> 0), mantissa
+  # round-up to c = 2, angle at the table edges and just below pi/2
+  w[0, :2] = [0, 0]
+  w[1, :2] = [0xFFFFFFFF, 0xFFFFFFFF]
+  w[2, :2] = [0x000FFE00, 0]
+  w[3, :2] = [0x000FFDFF, 0xFFFFFFFF]
+  w[4:8, 2:] = [[0, 0], [0x3FCFFFFF, 0xFFFFFFFF], [0x00F00000, 0],
+                [0xFFCFFFFF, 0xFFFFFFFF]]
+  fast, ref = _normals64(w)
+  assert np.isfinite(fast).all()
+  scale = np.maximum(1.0, np.abs(ref))
+  assert np.max(np.abs(fast - ref) / scale) < 4e-15
+  host, r = _bm64_host(w)
+  assert np.max(np.abs(fast - host) / np.maximum(1.0, r)[:, None]) < 1e-14
+  # r near 0 keeps relative accuracy (u1 -> 1: ln(c/2) = 0 exactly)
+  small = r < 1e-3
+  if small.any():
+    rel = np.abs(np.hypot(fast[small, 0], fast[small, 1]) / r[small] - 1)
+    assert rel.max() < 1e-14
+
+
+def test_bm64_normals_are_standard_normal():
+  """Distribution of the production normals: moments, tail mass beyond the
+  fp32 form's 5.77 sigma cut, and a Kolmogorov-Smirnov test."""
+  import scipy.stats
+  rng = np.random.RandomState(5)
+  n = 1 << 22
+  w = rng.randint(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+  fast, _ = _normals64(w)
+  z = fast.reshape(-1)
+  m = z.size
+  assert abs(z.mean()) < 5 / np.sqrt(m)
+  assert abs(z.var() - 1) < 5 * np.sqrt(2 / m)
+  assert abs(scipy.stats.skew(z)) < 5 * np.sqrt(6 / m)
+  assert abs(scipy.stats.kurtosis(z)) < 5 * np.sqrt(24 / m)
+  # P(|z| > 4) = 6.33e-5: binomial 5-sigma band
+  p4 = 2 * scipy.stats.norm.sf(4)
+  k4 = np.sum(np.abs(z) > 4)
+  assert abs(k4 - m * p4) < 5 * np.sqrt(m * p4)
+  assert scipy.stats.kstest(z[:1 << 21], 'norm').pvalue > 1e-3
+  # the two normals of a pair are uncorrelated
+  assert abs(np.corrcoef(fast[:, 0], fast[:, 1])[0, 1]) < 5 / np.sqrt(n)
