@@ -14,9 +14,11 @@ region is exactly --steps steps (fused --steps-per-launch per kernel launch),
 bracketed by a barrier + device sync on both sides; the reported time is the
 max over ranks.  value = chains_per_gpu * n_gpus * steps / time.
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), chains
-sharded by global id with no collective in the data path; one RCCL
-all-gather of the per-chain moments at collection (timed separately).
+Multi-GPU (weak scaling): one process per GPU (torch.distributed.run
+launches them; nothing here imports torch), chains sharded by global id with
+no collective in the data path; rank 0 hands its ncclUniqueId to the others
+over TCP (stdlib), barriers and the max-over-ranks time are RCCL all-reduces,
+and ONE RCCL all-gather collects the per-chain statistics (timed separately).
 """
 import argparse
 import json
@@ -64,28 +66,49 @@ def bytes_per_chain_step(d):
   return 8.0 * d + 8.0 + 1.0 / 8.0
 
 
-def cpu_baseline(budget_s=12.0):
-  """The oracle (NumPy restatement of the reference, bit-exact per chain)
-  timed on this host, including its legacy-MT19937 stream generation, on a
-  bounded sample of the cfg2 workload."""
-  import oracle
-  spec = cfg2_spec()
-  n, t = 2048, 8
+def _cpu_slice(args):
+  """One process of the CPU baseline: cfg2 chain-steps of n chains through
+  the vectorised NumPy restatement until the time budget is spent."""
+  n, t, budget_s, seed = args
+  from oracle.vector_mh import cfg2_run
+  mu, sg = np.linspace(-1., 1., D), np.linspace(0.5, 2., D)
   done, t0 = 0, time.perf_counter()
-  reps = 0
-  while time.perf_counter() - t0 < budget_s:
-    seeds = np.arange(reps * n, (reps + 1) * n)
-    streams = oracle.legacy_streams(spec, seeds, t)
-    oracle.run_mh(spec, np.zeros((n, D)), streams)
+  while True:
+    cfg2_run(n, t, mu, sg, 0.5, seed + done)
     done += n * t
-    reps += 1
-  el = time.perf_counter() - t0
-  return {'value': done / el, 'unit': 'chain-steps/s', 'cores': 1,
+    el = time.perf_counter() - t0
+    if el >= budget_s:
+      return done, el
+
+
+def cpu_baseline(budget_s=6.0, chains=65536):
+  """cfg2 on this host's cores, timed BEFORE the GPU is touched (the worker
+  processes are forked from a process with no HIP state): the vectorised
+  NumPy restatement (oracle/vector_mh.py, the reference's per-step arithmetic
+  for all chains at once, every step recorded) at N = 65 536 on one core,
+  then split over P = min(16, cpu_count) processes (the box's CPU share).
+  The reference SP itself: 877 chain-steps/s on 1 core."""
+  import multiprocessing as mp
+  t = 16
+  one_done, one_el = _cpu_slice((chains, t, budget_s, 1))
+  ncpu = os.cpu_count() or 1
+  procs = max(1, min(16, ncpu))
+  per = -(-chains // procs)
+  ctx = mp.get_context('fork')
+  with ctx.Pool(procs) as pool:
+    res = pool.map(_cpu_slice, [(per, t, budget_s, 100 + i) for i in range(procs)])
+  rate_all = sum(d / e for d, e in res)
+  return {'value': rate_all, 'unit': 'chain-steps/s', 'cores': procs,
           'kind': 'port',
-          'sample': '{} chains x {} steps x {} reps of cfg2 through '
-                    'oracle.run_mh incl. per-chain RandomState streams, one '
-                    'process (the reference SP itself: 877 chain-steps/s on 1 '
-                    'core, BASELINE.md)'.format(n, t, reps)}
+          'single_core': one_done / one_el,
+          'sample': 'cfg2 (d = 10), oracle/vector_mh.py vectorised NumPy '
+                    'restatement, every step recorded: {} chains x {}-step '
+                    'runs for {:.0f} s on 1 core ({:.3g} chain-steps/s), then '
+                    '{} processes x {} chains for {:.0f} s each (os.cpu_count '
+                    '= {}); the reference SP: 877 chain-steps/s on 1 core '
+                    '(BASELINE.md)'.format(chains, t, budget_s,
+                                           one_done / one_el, procs, per,
+                                           budget_s, ncpu)}
 
 
 def measured_traffic(chains, launch_steps, rng, trace):
@@ -104,6 +127,61 @@ def measured_traffic(chains, launch_steps, rng, trace):
         t.get('steps_per_launch') == launch_steps):
       return t['bytes_per_launch']
   return None
+
+
+class EngineCollective:
+  """The engine's own RCCL collectives (pbh_rccl_*): the production path."""
+
+  def __init__(self, eng):
+    self.eng = eng
+
+  def allreduce_max(self, v):
+    return self.eng.rccl_allreduce_max(v)
+
+  def gather_stats(self):
+    return self.eng.rccl_allgather_stats()
+
+
+def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
+             trace=True, moments=False, seed=20261015):
+  """One rank of the bench (weak scaling: chains_per_gpu chains per rank):
+  shard the global chain ids, warm up, time exactly `steps` steps between
+  barriers, take the max over ranks, then collect the per-chain statistics
+  with the one all-gather.  eng: probayes_amd.Engine (or a CPU stand-in with
+  the same methods, tests/test_dist.py); col: EngineCollective (RCCL) or
+  dist.TcpCollective (world > 1), None for one rank."""
+  from probayes_amd.dist import shard
+  offset, n = shard(chains_per_gpu * world, rank, world)
+  eng.init_chains(np.zeros((n, D)), chain_offset=offset)
+  eng.set_rng(rng, seed=seed)
+  eng.set_collect(moments=moments or not trace)
+  if trace:
+    eng.alloc_trace(warmup + steps, 1)
+
+  def barrier():
+    eng.sync()
+    if col is not None:
+      col.allreduce_max(0.0)
+
+  if warmup:
+    eng.run(warmup, steps_per_launch=spl)
+  barrier()
+  t0 = time.perf_counter()
+  eng.run(steps, steps_per_launch=spl, sync=False)
+  eng.sync()
+  el = time.perf_counter() - t0
+  kern_ms, launches = eng.last_run_ms()
+  barrier()
+  out = {'n': n, 'offset': offset, 'el': el, 'kern_ms': kern_ms,
+         'launches': launches}
+  if col is not None:
+    out['el'] = col.allreduce_max(el)
+    t1 = time.perf_counter()
+    if trace and not moments:
+      eng.trace_stats(warmup, steps)   # device reduction of the timed steps
+    out['stats'] = col.gather_stats()
+    out['collect_ms'] = (time.perf_counter() - t1) * 1e3
+  return out
 
 
 def main():
@@ -132,52 +210,33 @@ def main():
   if world != args.gpus:
     raise SystemExit('--gpus {} but WORLD_SIZE {}'.format(args.gpus, world))
 
-  from probayes_amd import Engine   # loads libpbhip.so before any torch
-  spec = cfg2_spec()
-  n = args.chains
-  eng = Engine(spec, device=local)
-  from probayes_amd.dist import shard
-  offset, n = shard(n * world, rank, world)   # weak scaling: n chains / GPU
-  eng.init_chains(np.zeros((n, D)), chain_offset=offset)
-  eng.set_rng(args.rng, seed=20261015)
-  eng.set_collect(moments=args.moments or args.no_trace)
-  if not args.no_trace:
-    eng.alloc_trace(args.warmup + args.steps, 1)
+  # the CPU baseline runs first, before anything touches the GPU
+  cpu = None
+  if world == 1 and rank == 0 and not args.no_cpu_baseline:
+    cpu = cpu_baseline()
 
-  dist = None
+  from probayes_amd import Engine
+  eng = Engine(cfg2_spec(), device=local)
+  col = None
   if world > 1:
-    import torch.distributed as dist   # control plane only (gloo, CPU)
-    dist.init_process_group('gloo')
-    uid = [Engine.rccl_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    eng.rccl_init(rank, world, uid[0])
-
-  def barrier():
-    eng.sync()
-    if world > 1:
-      eng.rccl_allreduce_max(0.0)
-
+    # control plane: rank 0's ncclUniqueId over TCP (stdlib), then RCCL
+    from probayes_amd.dist import exchange_unique_id
+    addr = os.environ.get('MASTER_ADDR', '127.0.0.1')
+    port = int(os.environ.get('MASTER_PORT', '29500')) + 1
+    uid = exchange_unique_id(rank, world,
+                             Engine.rccl_unique_id() if rank == 0 else None,
+                             addr, port)
+    eng.rccl_init(rank, world, uid)
+    col = EngineCollective(eng)
   spl = args.steps_per_launch
-  if args.warmup:
-    eng.run(args.warmup, steps_per_launch=spl)
-  barrier()
-  t0 = time.perf_counter()
-  eng.run(args.steps, steps_per_launch=spl, sync=False)
-  eng.sync()
-  el = time.perf_counter() - t0
-  kern_ms, launches = eng.last_run_ms()
-  barrier()
-  if world > 1:
-    el = eng.rccl_allreduce_max(el)
-    t1 = time.perf_counter()
-    if not args.no_trace and not args.moments:
-      eng.trace_stats(args.warmup, args.steps)   # device reduction of the trace
-    eng.rccl_allgather_moments()
-    collect_ms = (time.perf_counter() - t1) * 1e3
-  else:
-    collect_ms = None
+  res = run_rank(eng, col, rank, world, args.chains, args.steps, args.warmup,
+                 spl, args.rng, trace=not args.no_trace, moments=args.moments)
+  n, el, kern_ms, launches = res['n'], res['el'], res['kern_ms'], res['launches']
+  collect_ms = res.get('collect_ms')
+  if 'stats' in res:   # every chain of every rank, once
+    assert int(res['stats']['counts'].sum()) == args.chains * world
 
-  total = float(n) * world * args.steps
+  total = float(args.chains) * world * args.steps
   value = total / el
   bpcs = 0.0 if args.no_trace else bytes_per_chain_step(D)
   chain_steps_per_launch = n * (args.steps / max(launches, 1))
@@ -206,19 +265,20 @@ def main():
                                     n, min(spl, args.steps), args.rng,
                                     not args.no_trace),
                      'bytes_per_chain_step': bpcs,
-                     'kernel': ('mh_pair_kernel<10, {}>' if not os.environ.get('PBH_NO_PAIR') else 'mh_kernel<10, {}, DIAG, GAUSS>').format(args.rng.upper()),
+                     'kernel': ('mh_pair_kernel<10, {}, MOM={}>'.format(
+                         args.rng.upper(), int(args.moments or args.no_trace))
+                         if not os.environ.get('PBH_NO_PAIR') else
+                         'mh_kernel<10, {}, DIAG, GAUSS>'.format(args.rng.upper())),
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),
     }
     if collect_ms is not None:
       line['rccl_allgather_ms'] = collect_ms
-    if world == 1 and not args.no_cpu_baseline:
-      line['cpu_baseline'] = cpu_baseline()
+    if cpu is not None:
+      line['cpu_baseline'] = cpu
     print(json.dumps(line), flush=True)
   eng.close()
-  if dist is not None:
-    dist.destroy_process_group()
 
 
 if __name__ == '__main__':

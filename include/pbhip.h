@@ -214,6 +214,12 @@ int pbh_get_trace(pbh_engine *eng, int64_t first, int64_t n, double *x,
 int pbh_get_moments(pbh_engine *eng, double *sum, double *sumsq,
                     int64_t *n_acc, int64_t *n_steps);
 int pbh_reset_moments(pbh_engine *eng);
+/* Per-(chain, dim) effective sample size of trace records [first, first +
+ * count) on the device: Geyer's initial positive sequence over the
+ * autocorrelations of each centred series (the estimator behind cfg5's
+ * ESS/s); ess [d][N] on the host (may be NULL).  The result
+ * also stays in the engine for pbh_rccl_allgather_stats.                    */
+int pbh_trace_ess(pbh_engine *eng, int64_t first, int64_t count, double *ess);
 /* The same per-chain statistics reduced on the device from trace records
  * [first, first + count) (PD summate + expectation over a recorded trace,
  * pd_utils.py:332-411, pd.py:373-407, without copying the trace to the
@@ -227,10 +233,17 @@ int pbh_trace_stats(pbh_engine *eng, int64_t first, int64_t count, double *sum,
 int pbh_rccl_unique_id(uint8_t id[128]);
 int pbh_rccl_init(pbh_engine *eng, int32_t rank, int32_t world,
                   const uint8_t id[128]);
-/* Gathers every rank's moments ([2d+1][N_local] doubles, n_acc as double)
- * into out [world][2d+1][N_local] on the host.  Every rank must hold the
- * same N_local (PBH_ERR_ARG otherwise; pad the chain set to shard evenly). */
-int pbh_rccl_allgather_moments(pbh_engine *eng, double *out);
+/* The largest N_local over the ranks (a collective: every rank calls it).  */
+int pbh_rccl_max_chains(pbh_engine *eng, int64_t *n_max);
+/* The one collective of the data path: gathers every
+ * rank's per-chain statistics into out[world][3d+1][n_max] on the host,
+ * rows sum[d], sumsq[d], n_acc, ess[d] (the moment buffers: in-kernel
+ * moments or pbh_trace_stats; ess: pbh_trace_ess, NaN before), and every
+ * rank's N_local into counts[world].  Ranks may hold different N_local (the
+ * ragged contiguous blocks of dist.shard): rank r's columns >= counts[r] are
+ * padding.  Every rank enters every collective whatever fails locally, and
+ * all ranks then return the same error.                                     */
+int pbh_rccl_allgather_stats(pbh_engine *eng, double *out, int64_t *counts);
 /* Max-reduces one double over ranks (bench timing).                         */
 int pbh_rccl_allreduce_max(pbh_engine *eng, double *value);
 int pbh_rccl_destroy(pbh_engine *eng);

@@ -102,7 +102,10 @@ SIGNATURES = {
     'pbh_rccl_unique_id': (ctypes.c_int, [_u8p]),
     'pbh_rccl_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
                                      ctypes.c_int32, _u8p]),
-    'pbh_rccl_allgather_moments': (ctypes.c_int, [ctypes.c_void_p, _dp]),
+    'pbh_rccl_max_chains': (ctypes.c_int, [ctypes.c_void_p, _i64p]),
+    'pbh_rccl_allgather_stats': (ctypes.c_int, [ctypes.c_void_p, _dp, _i64p]),
+    'pbh_trace_ess': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_int64, _dp]),
     'pbh_rccl_allreduce_max': (ctypes.c_int, [ctypes.c_void_p, _dp]),
     'pbh_rccl_destroy': (ctypes.c_int, [ctypes.c_void_p]),
     'pbh_check_accept': (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _dp, _dp,

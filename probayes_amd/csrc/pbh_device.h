@@ -242,8 +242,9 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 // in LDS: 1025 {-2 ln(c_j/2), 1/c_j} pairs and 257 {sin, cos} pairs, 20.5 KB.
 // About 45 VALU per pair.  Accuracy: tests/test_gpu_normals.py (libm form).
 // ---------------------------------------------------------------------------
-constexpr int kBm64LogN = 1025, kBm64ScN = 257;
-constexpr int kBm64Doubles = 2 * (kBm64LogN + kBm64ScN);   // 2564 doubles
+constexpr int kBm64LogN = 1025, kBm64ScN = 257, kExp2N = 64;
+constexpr int kBm64ExpOff = 2 * (kBm64LogN + kBm64ScN);   // 2^(i/64) table
+constexpr int kBm64Doubles = kBm64ExpOff + kExp2N;         // 2628 doubles
 
 __device__ __forceinline__ uint32_t hi32(double v) {
   return (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32);
@@ -304,6 +305,47 @@ __device__ __forceinline__ void bm64_pair(uint32_t x, uint32_t y, uint32_t z,
   const double a0 = rr * cs, a1 = rr * sn;
   z0 = from_words(hi32(a0) ^ (z & 0x80000000u), lo32(a0));
   z1 = from_words(hi32(a1) ^ ((z << 1) & 0x80000000u), lo32(a1));
+}
+
+// ln S of a positive normal double from the same LDS log table: S = 2^e m,
+// c_j = m rounded to 10 mantissa bits, ln S = (e + 1) ln 2 - (T_j + r q(r)) / 2
+// with T_j = -2 ln(c_j / 2), r = (m - c_j) / c_j (q as in bm64_pair).  About
+// 20 VALU; absolute error ~1e-16 (relative near S = 1 is not kept: used for
+// log-sum-exp sums S in [1, K], added to the max).
+__device__ __forceinline__ double ln_tab(double S, const double *tab) {
+  const uint32_t sh = hi32(S);
+  const int e1 = (int)((sh >> 20) & 0x7FFu) - 1022;
+  const uint32_t mh = 0x3FF00000u | (sh & 0xFFFFFu);
+  const uint32_t ch = (mh + 0x200u) & 0xFFFFFC00u;
+  const double2 lt = reinterpret_cast<const double2 *>(tab)[(ch - 0x3FF00000u) >> 10];
+  const double r = (from_words(mh, lo32(S)) - from_words(ch, 0u)) * lt.y;
+  double q = __builtin_fma(r, -0.4, 0.5);
+  q = __builtin_fma(q, r, -2.0 / 3.0);
+  q = __builtin_fma(q, r, 1.0);
+  q = __builtin_fma(q, r, -2.0);
+  const double de = (double)e1;
+  const double h = -0.5 * __builtin_fma(r, q, lt.x);
+  return __builtin_fma(de, 6.93147180369123816490e-01,
+                       __builtin_fma(de, 1.90821492927058770002e-10, h));
+}
+
+// exp(y) for y <= 0 (log-sum-exp terms): y = (n + i/64) ln 2 + r, |r| <=
+// ln2 / 128, exp(y) = 2^n 2^(i/64) poly5(r) from the 64-entry LDS table.
+// About 16 VALU, within 2 ulp; y < -745 gives 0.
+__device__ __forceinline__ double exp_tab(double y, const double *tab) {
+  y = __builtin_fmax(y, -746.0);                             // -inf -> 0
+  const double k = __builtin_rint(y * 92.332482616893656);   // 64 / ln 2
+  // ln2/64 = hi + lo, hi with 36 significant bits: k hi exact for |k| < 2^17
+  double r = __builtin_fma(-k, 0.010830424696223417, y);
+  r = __builtin_fma(-k, 2.572804622327669e-14, r);
+  double p = __builtin_fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  const int ki = (int)k;
+  const double t = tab[kBm64ExpOff + (ki & 63)];
+  return __builtin_ldexp(t * p, ki >> 6);
 }
 
 // The 14 spare bits of a bm64_pair block: x[31:20] << 2 | z[21:20].

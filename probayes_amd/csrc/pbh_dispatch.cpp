@@ -158,8 +158,79 @@ hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
   return hipGetLastError();
 }
 
+// Effective sample size of every (chain, dim) series of trace records
+// [first, first + count): Geyer's initial positive sequence on the
+// autocorrelations of the centred series, the estimator of
+// scripts/bench_workloads.py ess_ips (rho_k = ac_k / ac_0 with ac_k =
+// sum_t xc_t xc_{t+k}; pairs rho_{2j+1} + rho_{2j+2} summed up to the first
+// non-positive one; ess = T / (1 + 2 sum)).  One thread per series (a wave's
+// 64 series are 512 contiguous bytes per record); autocovariances are formed
+// 32 lags per pass from a register window, passes stop at the first
+// non-positive pair.
+constexpr int kEssLags = 32;
+
+__global__ void trace_ess_kernel(const double *tx, int64_t n, int32_t d,
+                                 int64_t first, int64_t T, double *ess) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = i / n, c = i % n;
+  if (k >= d) return;
+  const int64_t stride = (int64_t)d * n;
+  const double *xs = tx + (first * d + k) * n + c;
+  double mean = 0.;
+  for (int64_t t = 0; t < T; ++t) mean += xs[t * stride];
+  mean /= (double)T;
+  double ac0 = 0.;
+  for (int64_t t = 0; t < T; ++t) {
+    const double v = xs[t * stride] - mean;
+    ac0 = __builtin_fma(v, v, ac0);
+  }
+  const double inv0 = 1.0 / (ac0 > 1e-300 ? ac0 : 1e-300);
+  const int64_t m = (T - 1) / 2;   // pairs (lags 2j+1, 2j+2), j < m
+  double s = 0.;
+  bool done = m <= 0;
+  for (int64_t L0 = 1; !done; L0 += kEssLags) {   // lags L0 .. L0 + 31
+    double acc[kEssLags];
+#pragma unroll
+    for (int l = 0; l < kEssLags; ++l) acc[l] = 0.;
+    for (int64_t t = 0; t + L0 < T; ++t) {
+      const double a = xs[t * stride] - mean;
+#pragma unroll
+      for (int l = 0; l < kEssLags; ++l) {
+        const int64_t u = t + L0 + l;
+        const double b = u < T ? xs[u * stride] - mean : 0.;
+        acc[l] = __builtin_fma(a, b, acc[l]);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < kEssLags; l += 2) {
+      const int64_t j = (L0 + l - 1) / 2;   // pair index of lags L0+l, L0+l+1
+      if (!done) {
+        if (j >= m) {
+          done = true;
+        } else {
+          const double pr = acc[l] * inv0 + acc[l + 1] * inv0;
+          if (pr <= 0.) done = true;
+          else s += pr;
+        }
+      }
+    }
+  }
+  const double den = 1.0 + 2.0 * s;
+  ess[k * n + c] = (double)T / (den > 1e-12 ? den : 1e-12);
+}
+
+hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
+                            int64_t first, int64_t count, double *ess,
+                            hipStream_t st) {
+  const int64_t m = (int64_t)d * n;
+  hipLaunchKernelGGL(trace_ess_kernel, dim3((unsigned)((m + 255) / 256)),
+                     dim3(256), 0, st, tx, n, d, first, count, ess);
+  return hipGetLastError();
+}
+
 // The bm64 tables (pbh_device.h): {-2 ln(c_j / 2), 1 / c_j} for c_j = 1 + j /
-// 1024, j = 0..1024, then {sin, cos}(j (pi/2) / 256), j = 0..256.  Evaluated
+// 1024, j = 0..1024, then {sin, cos}(j (pi/2) / 256), j = 0..256, then
+// 2^(i/64), i = 0..63.  Evaluated
 // in long double (64-bit significand) and rounded once to double.
 void bm64_tables(double *out) {
   for (int j = 0; j < kBm64LogN; ++j) {
@@ -176,6 +247,7 @@ void bm64_tables(double *out) {
   }
   sc[2 * 256] = 1.0;   // sin(pi/2), cos(pi/2) = 0 exactly
   sc[2 * 256 + 1] = 0.0;
+  for (int i = 0; i < kExp2N; ++i) out[kBm64ExpOff + i] = (double)exp2l(i / 64.0L);
 }
 
 // Diagnostic: bm64_pair against the same construction through ocml's libm

@@ -61,12 +61,13 @@ struct pbh_engine {
   int64_t mom_steps = 0;
   // production fp64 normal tables (bm64, pbh_device.h), read into LDS
   double *bm64 = nullptr;
+  double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
   bool spin_sync = true;     // PBH_SYNC=block: hipStreamSynchronize instead
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
   bool gibbs_fast = true;    // PBH_GIBBS_FAST=0 keeps the ndtri kernel for Philox
   int gibbs_lanes = 0;       // PBH_GIBBS_LANES: lanes per chain of that kernel
-  int gmm_lanes = 2;         // PBH_GMM_LANES: lanes per chain of the GMM kernel
+  int gmm_lanes = 4;         // PBH_GMM_LANES: lanes per chain of the GMM kernel
   // MVN target on the host (for the production Gibbs tables)
   std::vector<double> mvn_mean, mvn_U;
   double mvn_const = 0.;
@@ -145,15 +146,9 @@ int check_ptr(const void *p, const char *name) {
   return p ? PBH_OK : fail(PBH_ERR_ARG, "%s must not be NULL", name);
 }
 
-__global__ void pack_moments(const double *sum, const double *sq,
-                             const int64_t *nacc, double *out, int64_t dn,
-                             int64_t n) {
+__global__ void nacc_to_f64(const int64_t *nacc, double *out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < dn) {
-    out[i] = sum[i];
-    out[dn + i] = sq[i];
-  }
-  if (i < n) out[2 * dn + i] = (double)nacc[i];
+  if (i < n) out[i] = (double)nacc[i];
 }
 
 void free_trace(pbh_engine *e) {
@@ -224,7 +219,7 @@ int pbh_destroy(pbh_engine *e) {
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
-  dfree(e->bm64);
+  dfree(e->bm64); dfree(e->ess);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -529,7 +524,13 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
     if (!rc) rc = dalloc(e->nacc, n);
     if (!rc) rc = dalloc(e->xo, (size_t)8 * n);
     if (!rc) rc = dalloc(e->gq, (size_t)(d + 1) * n);
+    if (!rc) rc = dalloc(e->ess, (size_t)d * n);
     if (rc) return rc;
+  }
+  {
+    std::vector<double> nan((size_t)d * n, std::nan(""));
+    HIP_TRY(hipMemcpy(e->ess, nan.data(), nan.size() * sizeof(double),
+                      hipMemcpyHostToDevice));
   }
   e->gq_valid = false;
   std::vector<double> xt((size_t)n * d);
@@ -957,6 +958,22 @@ int pbh_trace_stats(pbh_engine *e, int64_t first, int64_t count, double *sum,
   return PBH_OK;
 }
 
+int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  int64_t rec = 0;
+  pbh_trace_len(e, &rec);
+  if (first < 0 || count < 2 || first + count > rec)
+    return fail(PBH_ERR_ARG, "ESS needs >= 2 records inside [0, %lld), got [%lld, %lld)",
+                (long long)rec, (long long)first, (long long)(first + count));
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(pbh::launch_trace_ess(e->tx, e->n, e->d, first, count, e->ess, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (ess)
+    HIP_TRY(hipMemcpy(ess, e->ess, (size_t)e->d * e->n * sizeof(double),
+                      hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
 int pbh_reset_moments(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
@@ -992,55 +1009,88 @@ int pbh_rccl_init(pbh_engine *e, int32_t rank, int32_t world, const uint8_t id[1
   }
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
+  if (!e->scalar) {
+    int rc = dalloc(e->scalar, 4);   // the agreement / max-reduce scratch
+    if (rc) return rc;
+  }
   RCCL_TRY(ncclCommInitRank(&e->comm, world, uid, rank));
   e->rank = rank;
   e->world = world;
   return PBH_OK;
 }
 
-int pbh_rccl_allgather_moments(pbh_engine *e, double *out) {
-  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+namespace {
+
+// Every rank enters every collective of a gather, whatever failed locally: a
+// rank that cannot proceed contributes NaN to an all-reduce of (status,
+// count) and every rank then returns the same error -- no rank is left
+// waiting inside RCCL (a collective only some ranks enter never completes).
+int rccl_agree(pbh_engine *e, bool ok, int64_t n, int64_t *n_max, const char *what) {
+  double v[3] = {ok ? 0. : std::nan(""), (double)n, -(double)n};
+  HIP_TRY(hipMemcpy(e->scalar, v, sizeof v, hipMemcpyHostToDevice));
+  RCCL_TRY(ncclAllReduce(e->scalar, e->scalar, 3, ncclFloat64, ncclMax, e->comm,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(v, e->scalar, sizeof v, hipMemcpyDeviceToHost));
+  if (v[0] != v[0])
+    return fail(PBH_ERR_STATE, "%s: a rank could not take part (see its own error)", what);
+  if (n_max) *n_max = (int64_t)v[1];
+  return PBH_OK;
+}
+
+}  // namespace
+
+int pbh_rccl_max_chains(pbh_engine *e, int64_t *n_max) {
+  if (check_ptr(e, "engine") || check_ptr(n_max, "n_max")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
-  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   HIP_TRY(hipSetDevice(e->device));
-  const int64_t n = e->n, dn = (int64_t)e->d * n, cnt = 2 * dn + n;
-  {
-    // ncclAllGather needs one count on every rank: refuse ragged shards
-    // (a mismatch would hang the collective) -- max(n) == -max(-n)
-    int rc0 = e->scalar ? PBH_OK : dalloc(e->scalar, 1);
-    if (rc0) return rc0;
-    double lim[2] = {(double)n, -(double)n};
-    double *dl = nullptr;
-    rc0 = dalloc(dl, 2);
-    if (rc0) return rc0;
-    hipError_t err = hipMemcpy(dl, lim, sizeof lim, hipMemcpyHostToDevice);
-    ncclResult_t nr = ncclSuccess;
-    if (err == hipSuccess)
-      nr = ncclAllReduce(dl, dl, 2, ncclFloat64, ncclMax, e->comm, e->stream);
-    if (err == hipSuccess && nr == ncclSuccess) err = hipStreamSynchronize(e->stream);
-    if (err == hipSuccess && nr == ncclSuccess)
-      err = hipMemcpy(lim, dl, sizeof lim, hipMemcpyDeviceToHost);
-    dfree(dl);
-    if (nr != ncclSuccess)
-      return fail(PBH_ERR_RCCL, "chain-count check failed: %s", ncclGetErrorString(nr));
-    HIP_TRY(err);
-    if (lim[0] != -lim[1])
-      return fail(PBH_ERR_ARG,
-                  "all-gather needs equal chain counts on every rank (%g..%g)",
-                  -lim[1], lim[0]);
-  }
-  int rc = dalloc(e->gather_send, cnt);
-  if (!rc) rc = dalloc(e->gather_recv, (size_t)cnt * e->world);
+  return rccl_agree(e, e->x != nullptr, e->n, n_max, "pbh_rccl_max_chains");
+}
+
+int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out") || check_ptr(counts, "counts"))
+    return PBH_ERR_ARG;
+  if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
+  HIP_TRY(hipSetDevice(e->device));
+  // 1. agree on the padded width; a rank without chains stops everyone
+  int64_t nm = 0;
+  int rc = rccl_agree(e, e->x != nullptr, e->n, &nm, "pbh_rccl_allgather_stats");
   if (rc) return rc;
-  const int64_t m = std::max(dn, n);
-  hipLaunchKernelGGL(pack_moments, dim3((unsigned)((m + 255) / 256)), dim3(256),
-                     0, e->stream, e->msum, e->msq, e->nacc, e->gather_send, dn, n);
+  const int64_t n = e->n, d = e->d, rows = 3 * d + 2;   // + the count row
+  // 2. buffers (a failure is reported through the next agreement)
+  const bool ok = !dalloc(e->gather_send, (size_t)rows * nm) &&
+                  !dalloc(e->gather_recv, (size_t)rows * nm * e->world);
+  rc = rccl_agree(e, ok, n, nullptr, "pbh_rccl_allgather_stats (buffers)");
+  if (rc) return rc;
+  // 3. pack [rows][nm]: sum, sumsq, n_acc, ess, then the rank's count
+  HIP_TRY(hipMemsetAsync(e->gather_send, 0, (size_t)rows * nm * sizeof(double), e->stream));
+  const size_t pitch = (size_t)nm * sizeof(double);
+  HIP_TRY(hipMemcpy2DAsync(e->gather_send, pitch, e->msum, n * sizeof(double),
+                           n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
+  HIP_TRY(hipMemcpy2DAsync(e->gather_send + d * nm, pitch, e->msq, n * sizeof(double),
+                           n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
+  hipLaunchKernelGGL(nacc_to_f64, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                     0, e->stream, e->nacc, e->gather_send + 2 * d * nm, n);
   HIP_TRY(hipGetLastError());
-  RCCL_TRY(ncclAllGather(e->gather_send, e->gather_recv, (size_t)cnt,
+  HIP_TRY(hipMemcpy2DAsync(e->gather_send + (2 * d + 1) * nm, pitch, e->ess,
+                           n * sizeof(double), n * sizeof(double), d,
+                           hipMemcpyDeviceToDevice, e->stream));
+  const double cnt = (double)n;
+  HIP_TRY(hipMemcpyAsync(e->gather_send + (3 * d + 1) * nm, &cnt, sizeof cnt,
+                         hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  // 4. the one all-gather over xGMI
+  RCCL_TRY(ncclAllGather(e->gather_send, e->gather_recv, (size_t)rows * nm,
                          ncclFloat64, e->comm, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(out, e->gather_recv, (size_t)cnt * e->world * sizeof(double),
+  std::vector<double> all((size_t)rows * nm * e->world);
+  HIP_TRY(hipMemcpy(all.data(), e->gather_recv, all.size() * sizeof(double),
                     hipMemcpyDeviceToHost));
+  for (int r = 0; r < e->world; ++r) {
+    const double *src = all.data() + (size_t)r * rows * nm;
+    std::memcpy(out + (size_t)r * (rows - 1) * nm, src, (size_t)(rows - 1) * nm * sizeof(double));
+    counts[r] = (int64_t)src[(size_t)(rows - 1) * nm];
+  }
   return PBH_OK;
 }
 
@@ -1048,8 +1098,6 @@ int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
   if (check_ptr(e, "engine") || check_ptr(value, "value")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
   HIP_TRY(hipSetDevice(e->device));
-  int rc = e->scalar ? PBH_OK : dalloc(e->scalar, 1);
-  if (rc) return rc;
   HIP_TRY(hipMemcpy(e->scalar, value, sizeof(double), hipMemcpyHostToDevice));
   RCCL_TRY(ncclAllReduce(e->scalar, e->scalar, 1, ncclFloat64, ncclMax, e->comm,
                          e->stream));

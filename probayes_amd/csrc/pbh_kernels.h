@@ -105,6 +105,10 @@ hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
                               int32_t d, int64_t W, int64_t first,
                               int64_t count, double *sum, double *sumsq,
                               int64_t *nacc, hipStream_t s);
+// per-(chain, dim) initial-positive-sequence ESS of trace records
+hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
+                            int64_t first, int64_t count, double *ess,
+                            hipStream_t st);
 // Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
 void bm64_tables(double *out);
 // Legacy (NumPy RandomState) stream generation (pbh_legacy.hip).

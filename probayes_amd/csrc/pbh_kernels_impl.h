@@ -1091,14 +1091,16 @@ __device__ __forceinline__ void gather_u32(uint32_t v, uint32_t (&all)[L]) {
 }
 
 // filter of the ratio form for a state carried as (M, S): e = exp(M' - M)
-// S' / S in fp32 (within 3e-6 of the ratio wherever |M|, |M'| <= 698, K <= 7)
+// S' / S in fp32 (v_exp_f32 1 ulp, argument rounding 4.2e-8 |y| as in
+// accept_filter_lead, S' rcp(S) 3 roundings of 2^-24: within 3e-6 of the
+// ratio wherever |M|, |M'| <= 698, K <= 7)
 template <int LB>
 __device__ __forceinline__ Decision accept_filter_ms(double Mp, double Sp,
                                                      double M, double S,
                                                      uint32_t lead) {
   constexpr float w = 1.0f / (float)(1u << LB);
   const float e = __builtin_amdgcn_exp2f((float)((Mp - M) * 1.4426950408889634)) *
-                  (float)(Sp / S);
+                  ((float)Sp * __builtin_amdgcn_rcpf((float)S));
   const float tlo = (float)lead * w;
   const float thi = tlo + w;
   const bool inr = __builtin_fabs(Mp) <= 698. && __builtin_fabs(M) <= 698.;
@@ -1205,10 +1207,11 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
       const double M = part_max<L>(m);
       double e = 0.;
 #pragma unroll
-      for (int kk = 0; kk < KL; ++kk) e += fast_exp(v[kk] - M);
+      for (int kk = 0; kk < KL; ++kk) e += exp_tab(v[kk] - M, s_bmt);
       const double S = part_sum<L>(any ? e : 0.);   // in [1, K]
-      // the recorded v.prob; the sum is in [1, K], the production log serves
-      const double lpp = M + fast_log(S);
+      // the recorded v.prob: the table log of S in [1, K] (off the
+      // acceptance's dependency chain)
+      const double lpp = M + ln_tab(S, s_bmt);
       // ---- acceptance (identical in every lane of the group) ----
       bool acc;
       if (!a.has_pred && s == 0) {
@@ -1287,6 +1290,261 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
     if (p == 0) {
       a.lp[c] = lp;
       if (mom) a.nacc[c] += nacc;
+    }
+  }
+}
+// ---------------------------------------------------------------------------
+// Quad MH kernel for the Gaussian-mixture target (cfg5, production RNG,
+// K <= 4 components, D <= 4): one chain per QUAD of adjacent lanes (lane
+// 4 c + p), 16 chains per wavefront, so 32 768 chains fill 2 048 wavefronts
+// (2 per SIMD).  Every exchange inside a chain is a DPP quad_perm move (one
+// VALU per 32-bit word), not a cross-row permlane.
+//  * Draws: aligned groups of 4 steps; lane p draws step 4 G + p alone
+//    (bm64 fp64 normals, a 14-bit threshold lead from the spare bits) and
+//    the quad broadcasts the group's draws to every lane.
+//  * Density: lane p owns component p; M = max and S = sum of exp(v_k - M)
+//    over the quad (two xor rounds each, the same association in every
+//    lane); log-sum-exp = M + ln S.
+//  * Acceptance on (M, S) -- no log on the step-to-step chain (see
+//    accept_filter_ms); the recorded v.prob M + ln S of a group's 4 states
+//    is evaluated after the group, one state per lane, so each lane pays one
+//    table log per 4 steps.  Undecided steps (~1e-4) take the exact ratio
+//    form of (lp', lp) with both logs evaluated on the spot (the same
+//    function of the same (M, S) as the recorded values).
+// The draws, counters and decisions are those of mh_kernel's production
+// Gaussian path; densities differ from it by rounding only.
+// ---------------------------------------------------------------------------
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E;   // quad_perm [1,0,3,2], [2,3,0,1]
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double qperm_f64(double v) {
+  return from_words(qperm_u32<CTRL>(hi32(v)), qperm_u32<CTRL>(lo32(v)));
+}
+// quad_perm [q, q, q, q]: lane q's value in every lane of the quad
+template <int Q>
+__device__ __forceinline__ double qbcast_f64(double v) {
+  return qperm_f64<Q * 85>(v);
+}
+
+// The quad kernel's decision path in fp32: e = exp(M' - M) S32' / S32 with
+// S32 = sum_k exp2f(fp32((v_k - M) log2 e)).  Error where a decision can
+// hinge on it (e in [2^-15, 1], i.e. |M' - M| log2 e <= 15): the argument
+// rounding 4.2e-8 x 15 = 6.3e-7, each S32 within 5.1e-7 (K <= 4 terms: a
+// term 2^y errs by at most 4.1e-8 |y| 2^y + 1 ulp <= 8.2e-8, plus three
+// fp32 additions), rcp / products 1.8e-7: about 2.3e-6 < the 4e-6 margin.
+// Outside that range the decision is certain (thi <= 1 < e, or tlo >= 2^-14
+// > e) or the lead is 0 and the exact form decides.
+template <int LB>
+__device__ __forceinline__ Decision accept_filter_ms32(double Mp, float Sp,
+                                                       double M, float S,
+                                                       uint32_t lead) {
+  constexpr float w = 1.0f / (float)(1u << LB);
+  const float e = __builtin_amdgcn_exp2f((float)((Mp - M) * 1.4426950408889634)) *
+                  (Sp * __builtin_amdgcn_rcpf(S));
+  const float tlo = (float)lead * w;
+  const float thi = tlo + w;
+  const bool inr = __builtin_fabs(Mp) <= 698. && __builtin_fabs(M) <= 698.;
+  const bool af = thi <= e * 0.999996f;
+  const bool rf = tlo > e * 1.000004f;
+  return Decision{inr && af, !(inr && (af || rf))};
+}
+
+template <int CTRL>
+__device__ __forceinline__ float qperm_f32(float v) {
+  return __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_mov_dpp(
+                                       __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+template <int D, int K, bool MOM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void mh_gmm_quad_kernel(KArgs a) {
+  static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
+  constexpr int P = (D + 1) / 2;         // bm64 blocks per step
+  constexpr int LB = 14;                 // threshold lead bits (spare bits)
+  __shared__ double s_bmt[kBm64Doubles];
+  bm64_load(s_bmt, a.bm64);
+  const int lane = threadIdx.x & 63;
+  const int p = lane & 3;
+  const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t wave = gt >> 6;
+  const int64_t c = gt >> 2;
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int64_t chain = a.off + cc;
+  const uint64_t act_bits = __ballot(active && p == 0);
+
+  // this lane's component (a lane p >= K contributes exp(-inf) = 0)
+  const bool own = p < K;
+  const double cw = own ? a.tw[p] : 0.;
+  const double c0 = own ? a.tw[K + p] : -__builtin_inf();
+  double cmu[D], psc[D], plc[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    cmu[i] = own ? a.tb[p * D + i] : 0.;
+    psc[i] = cld(a.pscl, i);
+    plc[i] = cld(a.ploc, i);
+  }
+  double x[D], ms = 0., mq = 0.;   // moments of dim p (p < D)
+#pragma unroll
+  for (int i = 0; i < D; ++i) x[i] = a.x[i * a.n + cc];
+  const double lp0 = a.lp[cc];
+  double lm = lp0, ls = 1.0;   // the state's density as (M, S): lp = M + ln S
+  float ls32 = 1.0f;           // S of the state in fp32 (the decision path)
+  int64_t nacc = 0;
+  int ph = (int)((a.g0 + 1) % a.thin);
+  int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  const uint32_t xoff = (uint32_t)(((int64_t)(p < D ? p : 0) * a.n + cc) * 8);
+  double *txrow = a.tx + ri * D * a.n;   // record ri's rows (wave-uniform)
+  const int64_t rstride = (int64_t)D * a.n;
+  __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
+
+  const int64_t gend = a.g0 + a.n_steps;
+  for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
+    // ---- lane p draws step 4 G + p; the quad shares the group's draws
+    double rown[D];
+    uint32_t lown = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const u32x4 w = philox4x32_10(ctr(q, 4 * G + p, chain), a.seed_lo, a.seed_hi);
+      double z0, z1;
+      bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
+      rown[2 * q] = z0;
+      if (2 * q + 1 < D) rown[2 * q + 1] = z1;
+      if (q == 0) lown = bm64_spare(w.x, w.z);
+    }
+    double gm[4], gs[4];     // the group's states (M, S), for the records
+    int64_t grec[4];
+    // one step of the group; j is a compile-time constant (DPP controls)
+    auto step = [&](auto J) {
+      constexpr int j = decltype(J)::value;
+      double r[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
+      const uint32_t lead = qperm_u32<j * 85>(lown);
+      const int64_t g = 4 * G + j;
+      grec[j] = -1;
+      gm[j] = lm;
+      gs[j] = ls;
+      if (g < a.g0 || g >= gend) return;   // wave-uniform
+      const int s = (int)(g - a.g0);
+      double xp[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) xp[i] = x[i] + __builtin_fma(r[i], psc[i], plc[i]);
+      double v = c0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const double u = (xp[i] - cmu[i]) * cw;
+        v = __builtin_fma(-u, u, v);
+      }
+      double M = __builtin_fmax(v, qperm_f64<kQuadXor1>(v));
+      M = __builtin_fmax(M, qperm_f64<kQuadXor2>(M));
+      const double dv = v - M;
+      // decision path: S in fp32 from v_exp_f32 (accept_filter_ms32)
+      float e32 = own ? __builtin_amdgcn_exp2f((float)(dv * 1.4426950408889634)) : 0.f;
+      e32 = e32 + qperm_f32<kQuadXor1>(e32);
+      const float S32 = e32 + qperm_f32<kQuadXor2>(e32);
+      // record path (off the decision's chain): S in fp64
+      double e = own ? exp_tab(dv, s_bmt) : 0.;
+      e = e + qperm_f64<kQuadXor1>(e);
+      const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
+      bool acc;
+      if (!a.has_pred && s == 0) {
+        acc = true;                                  // s = None on step 1
+      } else {
+        const Decision dc = a.acc_beta == 1.0
+            ? accept_filter_ms32<LB>(M, S32, lm, ls32, lead)
+            : accept_filter_lead<LB>((M + ln_tab(S, s_bmt)) * a.acc_beta,
+                                     (lm + ln_tab(ls, s_bmt)) * a.acc_beta,
+                                     lead, false);
+        acc = dc.acc;
+        if (__ballot(dc.need)) {   // wave-uniform, rare
+          if (dc.need) {
+            const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+            const double t = u01((lead << (32 - LB)) | (w.x >> LB), w.y);
+            const double lpp = M + ln_tab(S, s_bmt);
+            const double lpc = lm == lp0 && ls == 1.0 ? lp0 : lm + ln_tab(ls, s_bmt);
+            acc = ratio_accept(lpp * a.acc_beta, lpc * a.acc_beta, t, false, a.log_npi);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
+      lm = acc ? M : lm;
+      ls = acc ? S : ls;
+      ls32 = acc ? S32 : ls32;
+      gm[j] = lm;
+      gs[j] = ls;
+      if constexpr (MOM) {
+        nacc += acc ? 1 : 0;
+        double xo = x[0];
+#pragma unroll
+        for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
+        ms += xo;
+        mq = __builtin_fma(xo, xo, mq);
+      }
+      const bool rec_now = ph == 0;
+      const int64_t rec = ri;
+      double *row = txrow;
+      ph = (ph + 1 == a.thin) ? 0 : ph + 1;
+      if (ph == 0) {
+        ++ri;
+        txrow += rstride;
+      }
+      if (rec_now && rec >= 0 && rec < a.rec_cap) {
+        grec[j] = rec;
+        if (active && p < D) {
+          double xo = x[0];
+#pragma unroll
+          for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
+          st_buf(row, xoff, 0, xo);   // wave-uniform base
+        }
+        // the quad agrees: bit 4 c of the ballot is chain c's; compress the
+        // 16 chain bits of this wave (SALU)
+        uint64_t m = __ballot(acc) & 0x1111111111111111ull & act_bits;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0xFFFFull;
+        if (lane == 0 && wave < 4 * a.W)   // stay inside the record
+          reinterpret_cast<uint16_t *>(a.tacc)[rec * 4 * a.W + wave] = (uint16_t)m;
+      }
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    // ---- the group's recorded v.prob: lane p evaluates step 4 G + p's
+    double pm = gm[0], pss = gs[0];
+    int64_t prec = grec[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      pm = p == j ? gm[j] : pm;
+      pss = p == j ? gs[j] : pss;
+      prec = p == j ? grec[j] : prec;
+    }
+    if (prec >= 0 && active) {
+      const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
+      __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + c]);
+    }
+  }
+  if (active) {
+    if (p < D) {
+      double xo = x[0];
+#pragma unroll
+      for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
+      a.x[p * a.n + c] = xo;
+      if constexpr (MOM) {
+        a.msum[p * a.n + c] += ms;
+        a.msq[p * a.n + c] += mq;
+      }
+    }
+    if (p == 0) {
+      a.lp[c] = lm == lp0 && ls == 1.0 ? lp0 : lm + ln_tab(ls, s_bmt);
+      if constexpr (MOM) a.nacc[c] += nacc;
     }
   }
 }
@@ -1907,9 +2165,9 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
   if constexpr (D <= 4) {
     if (a.target == PBH_TARGET_GMM && a.prop == PBH_PROP_GAUSS) {
       if (gmm_pair_form(a) && a.tn >= 2 && a.tn <= 4) {
-        // lanes per chain: PBH_GMM_LANES (2 or 4), default 2 (measured:
-        // 4 lanes, each repeating the Philox block, are slower at cfg5)
-        const int L = a.gmm_lanes == 4 ? 4 : 2;
+        // lanes per chain: PBH_GMM_LANES = 4 (default: the quad kernel) or
+        // 2 (the lane-pair kernel, rows of 32 lanes)
+        const int L = a.gmm_lanes == 2 ? 2 : 4;
         const int64_t waves = (a.n + 64 / L - 1) / (64 / L);
         const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
         if (L == 2) {
@@ -1919,13 +2177,20 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
             hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 3, 2>), grid, block, 0, st, a);
           else
             hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 4, 2>), grid, block, 0, st, a);
+        } else if (a.moments) {
+          if (a.tn == 2)
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 2, true>), grid, block, 0, st, a);
+          else if (a.tn == 3)
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 3, true>), grid, block, 0, st, a);
+          else
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 4, true>), grid, block, 0, st, a);
         } else {
           if (a.tn == 2)
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 2, 4>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 2, false>), grid, block, 0, st, a);
           else if (a.tn == 3)
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 3, 4>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 3, false>), grid, block, 0, st, a);
           else
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 4, 4>), grid, block, 0, st, a);
+            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 4, false>), grid, block, 0, st, a);
         }
         return hipGetLastError();
       }

@@ -4,10 +4,21 @@ Chains are independent, so the data path has no collective: rank r of W runs
 the contiguous global chain ids [offset, offset + count) and keys its RNG by
 global id (Philox) or by seeds[offset:offset + count] (legacy replay), which
 makes every chain's trace identical for any W.  The single exchange is the
-collection of per-chain moments: an RCCL all-gather over xGMI issued by the
-engine (pbh_rccl_allgather_moments), or -- for CPU tests of this host logic
--- a torch.distributed gloo all-gather of the same [2d+1][count] block.
+collection of per-chain statistics: ONE RCCL all-gather over xGMI issued by
+the engine (pbh_rccl_allgather_stats: sum, sumsq, n_acc, ESS per chain,
+ragged shards padded to the largest).
+
+Control plane, standard library only (no torch): rank 0 hands its 128-byte
+ncclUniqueId to the other ranks over TCP (exchange_unique_id).  TcpCollective
+is the same star exchange carrying NumPy blocks; it stands in for the
+engine's RCCL calls in CPU tests of the rank logic (tests/test_dist.py) and
+packs blocks exactly like the engine (pack_stats / engine.unpack_stats).
 """
+import io
+import socket
+import struct
+import time
+
 import numpy as np
 
 
@@ -21,36 +32,144 @@ def shard(n_total, rank, world):
   return offset, count
 
 
-def pack_moments(sum_, sumsq, n_acc):
-  """[2d+1][N] block the engine's RCCL all-gather moves (pbhip.h)."""
+def pack_stats(sum_, sumsq, n_acc, ess=None, n_max=None):
+  """The [3d+1][n_max] block pbh_rccl_allgather_stats moves for one rank:
+  rows sum[d], sumsq[d], n_acc, ess[d] (NaN when absent), zero padding past
+  the rank's own count."""
   sum_, sumsq = np.asarray(sum_, np.float64), np.asarray(sumsq, np.float64)
-  return np.concatenate([sum_.T, sumsq.T,
-                         np.asarray(n_acc, np.float64)[None, :]], axis=0)
+  n, d = sum_.shape
+  n_max = n if n_max is None else int(n_max)
+  ess = np.full((n, d), np.nan) if ess is None else np.asarray(ess, np.float64)
+  blk = np.zeros((3 * d + 1, n_max))
+  blk[:, :n] = np.concatenate([sum_.T, sumsq.T,
+                               np.asarray(n_acc, np.float64)[None, :], ess.T])
+  return blk
 
 
-def unpack_gathered(blocks, d):
-  """[W][2d+1][n] gathered blocks -> chain-major (sum [N, d], sumsq, n_acc)."""
-  cat = np.concatenate(list(blocks), axis=1)
-  return cat[:d].T, cat[d:2 * d].T, cat[2 * d].astype(np.int64)
+# ---------------------------------------------------------------------------
+# TCP control plane (stdlib)
+# ---------------------------------------------------------------------------
+def _send_msg(sock, payload):
+  sock.sendall(struct.pack('<Q', len(payload)) + payload)
 
 
-class GlooCollective:
-  """torch.distributed (gloo, CPU) stand-in for the engine's RCCL calls."""
+def _recv_exact(sock, n):
+  buf = bytearray()
+  while len(buf) < n:
+    chunk = sock.recv(min(1 << 20, n - len(buf)))
+    if not chunk:
+      raise ConnectionError('peer closed the control connection')
+    buf += chunk
+  return bytes(buf)
 
-  def __init__(self):
-    import torch.distributed as dist
-    self.dist = dist
-    self.rank, self.world = dist.get_rank(), dist.get_world_size()
 
-  def allgather_blocks(self, block):
-    import torch
-    t = torch.from_numpy(np.ascontiguousarray(block))
-    outs = [torch.empty_like(t) for _ in range(self.world)]
-    self.dist.all_gather(outs, t)
-    return np.stack([o.numpy() for o in outs])
+def _recv_msg(sock):
+  (n,) = struct.unpack('<Q', _recv_exact(sock, 8))
+  return _recv_exact(sock, n)
+
+
+def _connect(addr, port, timeout):
+  t_end = time.monotonic() + timeout
+  while True:
+    try:
+      return socket.create_connection((addr, port), timeout=timeout)
+    except OSError:
+      if time.monotonic() > t_end:
+        raise
+      time.sleep(0.05)
+
+
+class TcpCollective:
+  """Star-topology exchange over TCP: rank 0 listens on (addr, port), the
+  other ranks connect and announce their rank.  Used for the ncclUniqueId
+  hand-off and, in CPU tests, in place of the engine's RCCL collectives."""
+
+  def __init__(self, rank, world, addr='127.0.0.1', port=29511, timeout=120.0):
+    self.rank, self.world = int(rank), int(world)
+    self.peers = {}
+    self.sock = None
+    if self.world == 1:
+      return
+    if self.rank == 0:
+      srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+      srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+      srv.bind((addr, port))
+      srv.listen(self.world)
+      srv.settimeout(timeout)
+      try:
+        while len(self.peers) < self.world - 1:
+          conn, _ = srv.accept()
+          conn.settimeout(timeout)
+          (r,) = struct.unpack('<i', _recv_exact(conn, 4))
+          self.peers[r] = conn
+      finally:
+        srv.close()
+    else:
+      self.sock = _connect(addr, port, timeout)
+      self.sock.sendall(struct.pack('<i', self.rank))
+
+  def bcast_bytes(self, payload):
+    """rank 0's payload on every rank."""
+    if self.world == 1:
+      return payload
+    if self.rank == 0:
+      for conn in self.peers.values():
+        _send_msg(conn, payload)
+      return payload
+    return _recv_msg(self.sock)
+
+  def allgather(self, arr):
+    """[world, ...] stack of every rank's equally shaped array."""
+    if self.world == 1:
+      return np.asarray(arr)[None]
+    buf = io.BytesIO()
+    np.save(buf, np.ascontiguousarray(arr), allow_pickle=False)
+    if self.rank == 0:
+      parts = {0: buf.getvalue()}
+      for r, conn in self.peers.items():
+        parts[r] = _recv_msg(conn)
+      blob = b''.join(struct.pack('<Q', len(parts[r])) + parts[r]
+                      for r in range(self.world))
+      for conn in self.peers.values():
+        _send_msg(conn, blob)
+    else:
+      _send_msg(self.sock, buf.getvalue())
+      blob = _recv_msg(self.sock)
+    out, pos = [], 0
+    for _ in range(self.world):
+      (n,) = struct.unpack('<Q', blob[pos:pos + 8])
+      out.append(np.load(io.BytesIO(blob[pos + 8:pos + 8 + n]),
+                         allow_pickle=False))
+      pos += 8 + n
+    return np.stack(out)
 
   def allreduce_max(self, value):
-    import torch
-    t = torch.tensor([float(value)], dtype=torch.float64)
-    self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-    return float(t.item())
+    return float(self.allgather(np.array([float(value)])).max())
+
+  def allgather_stats(self, sum_, sumsq, n_acc, ess=None):
+    """The engine's pbh_rccl_allgather_stats contract on the CPU: the
+    padded [world][3d+1][n_max] block and every rank's count."""
+    n = np.asarray(sum_).shape[0]
+    counts = self.allgather(np.array([n], np.int64))[:, 0]
+    blk = pack_stats(sum_, sumsq, n_acc, ess, n_max=int(counts.max()))
+    return self.allgather(blk), counts
+
+  def close(self):
+    for conn in self.peers.values():
+      conn.close()
+    if self.sock is not None:
+      self.sock.close()
+    self.peers, self.sock = {}, None
+
+
+def exchange_unique_id(rank, world, uid=None, addr='127.0.0.1', port=29511,
+                       timeout=120.0):
+  """rank 0's ncclUniqueId (128 bytes) on every rank, over TCP."""
+  col = TcpCollective(rank, world, addr, port, timeout)
+  try:
+    got = col.bcast_bytes(bytes(uid) if rank == 0 else b'')
+  finally:
+    col.close()
+  if len(got) != 128:
+    raise ValueError('ncclUniqueId must be 128 bytes, got {}'.format(len(got)))
+  return got

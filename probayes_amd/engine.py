@@ -67,6 +67,17 @@ def mvn_psd(mean, cov):
   return _f64(co._LP), float(const)
 
 
+def unpack_stats(out, counts, d):
+  """[world][3d+1][n_max] gather block (pbh_rccl_allgather_stats) -> the
+  per-chain statistics of all ranks concatenated in rank (= global chain)
+  order, padding columns dropped."""
+  cols = [out[r, :, :counts[r]] for r in range(len(counts))]
+  a = np.concatenate(cols, axis=1) if cols else np.empty((3 * d + 1, 0))
+  return {'sum': a[:d].T.copy(), 'sumsq': a[d:2 * d].T.copy(),
+          'n_acc': a[2 * d].astype(np.int64), 'ess': a[2 * d + 1:].T.copy(),
+          'counts': np.asarray(counts, np.int64)}
+
+
 class Engine:
   """One libpbhip engine on one device, running one lowered model."""
 
@@ -327,11 +338,28 @@ class Engine:
     _lib.call('pbh_rccl_init', self._h, int(rank), int(world), buf)
     self.world = int(world)
 
-  def rccl_allgather_moments(self):
-    d, n = self.dim, self.n
-    out = np.empty((self.world, 2 * d + 1, n))
-    _lib.call('pbh_rccl_allgather_moments', self._h, _dp(out))
-    return out
+  def rccl_allgather_stats(self):
+    """The one RCCL all-gather: every rank's per-chain statistics, in
+    global chain order (ranks hold contiguous blocks, dist.shard).  Returns
+    {'sum': [N, d], 'sumsq': [N, d], 'n_acc': [N], 'ess': [N, d],
+    'counts': [world]}; ess is NaN for a rank that never ran trace_ess."""
+    d = self.dim
+    nm = _c.c_int64()
+    _lib.call('pbh_rccl_max_chains', self._h, _c.byref(nm))
+    out = np.empty((self.world, 3 * d + 1, nm.value))
+    counts = np.empty(self.world, np.int64)
+    _lib.call('pbh_rccl_allgather_stats', self._h, _dp(out),
+              counts.ctypes.data_as(_c.POINTER(_c.c_int64)))
+    return unpack_stats(out, counts, d)
+
+  def trace_ess(self, first=0, count=None):
+    """Per-chain, per-dim initial-positive-sequence ESS of trace records
+    [first, first + count), computed on the device: [N, d]."""
+    count = self.trace_len() - first if count is None else count
+    out = np.empty((self.dim, self.n))
+    _lib.call('pbh_trace_ess', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(count)), _dp(out))
+    return out.T.copy()
 
   def rccl_allreduce_max(self, value):
     v = _c.c_double(float(value))

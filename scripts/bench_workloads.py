@@ -5,8 +5,9 @@
         log ufun, joint prior), 128 chains -- and a 65 536-chain run
   cfg3  8-dim mvn CondCov Gibbs, 32 768 chains, 8 x 256 coordinate steps
   cfg5  3-component 2-D GMM, 32 768 chains (the per-GPU share of 262 144),
-        2 000 steps, ESS/s (initial-positive-sequence ESS, min over dims,
-        summed over chains, / kernel wall time)
+        2 000 steps, ESS/s (initial-positive-sequence ESS computed on the
+        device from the resident trace, min over dims, summed over chains, /
+        kernel time)
   lik   likelihoods.py bool_perm_freq: 2^28 rows x 2 columns (naive-Bayes
         table shape of examples/naive), HBM read stream
   legacy  cfg2 in the reference-identical REPLAY mode: the per-chain NumPy
@@ -83,6 +84,7 @@ def run(name, n, steps, rng='philox', spl=0, trace=True):
   init = oracle.workloads.golden_init(name, n)
   eng.init_chains(init)
   eng.set_rng(rng, seed=11)
+  eng.set_collect(moments=not trace)   # with a trace: device trace_stats
   eng.run(8)          # warm-up launch (code-object load stays untimed)
   if trace:
     eng.alloc_trace(steps, 1)
@@ -240,15 +242,17 @@ def main():
     for line in lines:
       print(json.dumps(line), flush=True)
     return
+  # ESS on the device from the resident trace (no host copy of it):
+  # pbh_trace_ess, Geyer's initial positive sequence per chain and dim
   t0 = time.perf_counter()
-  tr = eng.trace()
+  ess_dev = eng.trace_ess(500)
+  o['ess_device_s'] = time.perf_counter() - t0
   eng.close()
-  ess = [ess_ips(tr['v_x'][:, 500:, k]).sum() for k in range(2)]
-  o['ess_min_dim'] = float(min(ess))
+  ess = ess_dev.sum(axis=0)
+  o['ess_min_dim'] = float(ess.min())
   o['ess_per_s'] = o['ess_min_dim'] / (o['kernel_ms'] / 1e3)
-  o['ess_host_s'] = time.perf_counter() - t0
   o['roofline'] = roofline(2 * 8 + 8 + 1 / 8, 32768 * 2000, o['kernel_ms'],
-                           'mh_gmm_lanes_kernel<2, 3, 2>')
+                           'mh_gmm_quad_kernel<2, 3>' if os.environ.get('PBH_GMM_LANES', '4') != '2' else 'mh_gmm_lanes_kernel<2, 3, 2>')
   if cpu:
     o['cpu_baseline'] = cpu_chain_rate('gmm2', 512, 8, args.cpu_budget)
   lines.append(dict(o, config='cfg5 per-GPU share'))

@@ -1,6 +1,11 @@
-"""Multi-GPU host logic on CPU: world_size-2 gloo processes shard the chains
-by global id, run their shard, and gather the per-chain moments; the result
-must equal the unsharded run (SURVEY.md §8(e) invariance)."""
+"""Multi-GPU host logic on CPU: world-2 processes run
+bench.py's own rank logic (bench.run_rank: shard -> run -> device trace
+statistics -> the one all-gather -> max-over-ranks time) with a CPU stand-in
+for the engine (the oracle, bit-exact per chain, keyed by global chain id)
+and the stdlib TCP collective in place of RCCL; the gathered statistics must
+equal those of the unsharded run.  Also: the ncclUniqueId hand-off and the
+ragged gather contract of pbh_rccl_allgather_stats (pad to the largest
+shard, counts alongside)."""
 import os
 import socket
 import subprocess
@@ -9,7 +14,8 @@ import sys
 import numpy as np
 import pytest
 
-from probayes_amd.dist import shard, pack_moments, unpack_gathered
+from probayes_amd.dist import shard, pack_stats, TcpCollective
+from probayes_amd.engine import unpack_stats
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -27,49 +33,97 @@ def test_shard_partition():
     shard(10, 2, 2)
 
 
-def test_pack_unpack_roundtrip():
+def test_pack_unpack_ragged_roundtrip():
+  """pbh_rccl_allgather_stats' block layout: [world][3d+1][n_max] with zero
+  padding past each rank's count; unpack_stats drops the padding and
+  concatenates ranks in global chain order."""
   rs = np.random.RandomState(0)
-  s, q, a = rs.normal(size=(5, 3)), rs.normal(size=(5, 3)), rs.randint(0, 9, 5)
-  blk = pack_moments(s, q, a)
-  s2, q2, a2 = unpack_gathered([blk[:, :2], blk[:, 2:]], 3)
-  np.testing.assert_array_equal(s2, s)
-  np.testing.assert_array_equal(q2, q)
-  np.testing.assert_array_equal(a2, a)
+  d, counts = 3, np.array([5, 4, 4])
+  full = {'sum': rs.normal(size=(13, d)), 'sumsq': rs.normal(size=(13, d)),
+          'n_acc': rs.randint(0, 9, 13), 'ess': rs.uniform(1, 9, (13, d))}
+  blocks, o = [], 0
+  for c in counts:
+    sl = slice(o, o + c)
+    blocks.append(pack_stats(full['sum'][sl], full['sumsq'][sl],
+                             full['n_acc'][sl], full['ess'][sl], n_max=5))
+    o += c
+  got = unpack_stats(np.stack(blocks), counts, d)
+  for k in ('sum', 'sumsq', 'n_acc', 'ess'):
+    np.testing.assert_array_equal(got[k], full[k])
+  assert np.isnan(pack_stats(full['sum'], full['sumsq'], full['n_acc'])[2 * d + 1:]).all()
 
 
-WORKER = r'''
-import os, sys, numpy as np
-sys.path.insert(0, {root!r}); sys.path.insert(0, os.path.join({root!r}, 'tests'))
-import torch.distributed as dist
-dist.init_process_group('gloo')
+ENGINE_STANDIN = r'''
+import os, sys, time, numpy as np
+sys.path.insert(0, {root!r})
 import oracle
-from probayes_amd.dist import shard, pack_moments, unpack_gathered, GlooCollective
-rank, world = dist.get_rank(), dist.get_world_size()
-spec = oracle.golden_spec('gmm2')
-N, T = 37, 40
-seeds = np.arange(1000, 1000 + N)
-off, cnt = shard(N, rank, world)
-out = oracle.run_mh(spec, np.zeros((cnt, 2)),
-                    oracle.legacy_streams(spec, seeds[off:off + cnt], T))
-x = out['v_x']
-blk = pack_moments(x.sum(1), (x * x).sum(1), out['u'].sum(1))
-col = GlooCollective()
-# ragged shards: pad to the max count for the fixed-size all-gather
-m = shard(N, 0, world)[1]
-pad = np.zeros((blk.shape[0], m)); pad[:, :cnt] = blk
-g = col.allgather_blocks(pad)
-blocks = [g[r][:, :shard(N, r, world)[1]] for r in range(world)]
-s, q, a = unpack_gathered(blocks, 2)
-tmax = col.allreduce_max(float(rank))
+
+class OracleEngine:
+  """CPU stand-in with the Engine methods bench.run_rank calls: every chain
+  is the reference's (oracle.run_mh over per-chain legacy streams seeded by
+  its GLOBAL id), so a rank's block equals the same block of an unsharded
+  run."""
+  def __init__(self, spec):
+    self.spec = spec
+  def init_chains(self, x0, chain_offset=0):
+    self.x0, self.off = np.asarray(x0, float), int(chain_offset)
+  def set_rng(self, rng, seed=0):
+    self.seed = int(seed)
+  def set_collect(self, moments=True):
+    self.moments = moments
+  def alloc_trace(self, cap, thin=1):
+    self.cap, self.done = cap, 0
+  def run(self, n, steps_per_launch=0, sync=True):
+    self.done += n
+  def sync(self):
+    pass
+  def last_run_ms(self):
+    return 1.0, 1
+  def trace_stats(self, first, count):
+    n = len(self.x0)
+    seeds = self.seed + self.off + np.arange(n)
+    out = oracle.run_mh(self.spec, self.x0,
+                        oracle.legacy_streams(self.spec, seeds, self.done))
+    x = out['v_x'][:, first:first + count]
+    self.stats = (x.sum(1), (x * x).sum(1), out['u'][:, first:first + count].sum(1))
+    return self.stats
+'''
+
+WORKER = ENGINE_STANDIN + r'''
+sys.path.insert(0, os.path.join({root!r}, 'tests'))
+import bench
+from probayes_amd.dist import TcpCollective
+from probayes_amd.engine import unpack_stats
+rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+col = TcpCollective(rank, world, '127.0.0.1', int(os.environ['MASTER_PORT']))
+
+class Col:
+  """TcpCollective with the EngineCollective interface of bench.py"""
+  def allreduce_max(self, v):
+    return col.allreduce_max(v)
+  def gather_stats(self):
+    s, q, a = eng.stats
+    blk, counts = col.allgather_stats(s, q, a)
+    return unpack_stats(blk, counts, bench.D)
+
+eng = OracleEngine(bench.cfg2_spec())
+res = bench.run_rank(eng, Col(), rank, world, chains_per_gpu=6, steps=12,
+                     warmup=5, spl=4, rng='philox', seed=300)
+st = res['stats']
 if rank == 0:
-  full = oracle.run_mh(spec, np.zeros((N, 2)), oracle.legacy_streams(spec, seeds, T))
-  fx = full['v_x']
-  assert np.array_equal(s, fx.sum(1)), 'sum'
-  assert np.array_equal(q, (fx * fx).sum(1)), 'sumsq'
-  assert np.array_equal(a, full['u'].sum(1)), 'n_acc'
-  assert tmax == world - 1
+  ref = OracleEngine(bench.cfg2_spec())
+  ref.init_chains(np.zeros((6 * world, bench.D)), 0)
+  ref.set_rng('philox', 300)
+  ref.alloc_trace(17)
+  ref.run(17)
+  s, q, a = ref.trace_stats(5, 12)
+  assert np.array_equal(st['sum'], s), 'sum'
+  assert np.array_equal(st['sumsq'], q), 'sumsq'
+  assert np.array_equal(st['n_acc'], a), 'n_acc'
+  assert list(st['counts']) == [6] * world
+  assert res['el'] >= 0 and res['offset'] == 0
   print('DIST_OK')
-dist.destroy_process_group()
+col.close()
 '''
 
 
@@ -81,17 +135,56 @@ def _free_port():
   return p
 
 
-def test_two_rank_gloo_sharded_run_matches_unsharded(tmp_path):
-  script = tmp_path / 'worker.py'
-  script.write_text(WORKER.format(root=ROOT))
-  port = _free_port()
+def _spawn(script, world, port):
   procs = []
-  for r in range(2):
-    env = dict(os.environ, RANK=str(r), WORLD_SIZE='2', LOCAL_RANK=str(r),
-               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  for r in range(world):
+    env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world),
+               LOCAL_RANK=str(r), MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(port))
     procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
                                   stdout=subprocess.PIPE,
                                   stderr=subprocess.STDOUT, text=True))
   outs = [p.communicate(timeout=240)[0] for p in procs]
   assert all(p.returncode == 0 for p in procs), outs
+  return outs
+
+
+def test_two_rank_bench_rank_logic_matches_unsharded(tmp_path):
+  script = tmp_path / 'worker.py'
+  script.write_text(WORKER.format(root=ROOT))
+  outs = _spawn(script, 2, _free_port())
   assert 'DIST_OK' in outs[0], outs
+
+
+UID_WORKER = r'''
+import os, sys
+sys.path.insert(0, {root!r})
+from probayes_amd.dist import exchange_unique_id, TcpCollective
+rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+port = int(os.environ['MASTER_PORT'])
+uid = bytes(range(128)) if rank == 0 else None
+got = exchange_unique_id(rank, world, uid, '127.0.0.1', port)
+assert got == bytes(range(128))
+# ragged all-gather of statistics (counts 4, 3, 3 for 10 chains)
+import numpy as np
+from probayes_amd.dist import shard
+off, n = shard(10, rank, world)
+col = TcpCollective(rank, world, '127.0.0.1', port + 1)
+s = np.arange(off, off + n, dtype=float)[:, None] * np.ones((1, 2))
+blk, counts = col.allgather_stats(s, s * s, np.arange(off, off + n))
+assert list(counts) == [shard(10, r, world)[1] for r in range(world)]
+assert blk.shape == (world, 7, max(counts))
+from probayes_amd.engine import unpack_stats
+u = unpack_stats(blk, counts, 2)
+assert np.array_equal(u['n_acc'], np.arange(10))
+assert col.allreduce_max(rank) == world - 1
+col.close()
+print('UID_OK', rank)
+'''
+
+
+def test_unique_id_handoff_and_ragged_gather_three_ranks(tmp_path):
+  script = tmp_path / 'uid.py'
+  script.write_text(UID_WORKER.format(root=ROOT))
+  outs = _spawn(script, 3, _free_port())
+  assert all('UID_OK' in o for o in outs), outs

@@ -184,22 +184,79 @@ def test_engine_errors_are_loud():
 
 
 def test_rccl_single_rank_allgather_and_max():
-  """The engine's RCCL path (one rank: the GPU box has one card)."""
+  """The engine's RCCL path (one rank: the GPU box has one card): the stats
+  gather returns the engine's moments, the device ESS rows and the count."""
   from probayes_amd import Engine
   spec = _diag10_spec()
   eng = Engine(spec)
   eng.init_chains(np.zeros((1000, 10)))
   eng.set_rng('philox', 3)
-  eng.run(20)
+  eng.alloc_trace(40, 1)
+  eng.run(40)
   eng.rccl_init(0, 1, Engine.rccl_unique_id())
-  g = eng.rccl_allgather_moments()
+  g = eng.rccl_allgather_stats()
+  assert np.isnan(g['ess']).all()          # no pbh_trace_ess yet
   m = eng.moments()
-  assert g.shape == (1, 21, 1000)
-  np.testing.assert_array_equal(g[0, :10].T, m['sum'])
-  np.testing.assert_array_equal(g[0, 10:20].T, m['sumsq'])
-  np.testing.assert_array_equal(g[0, 20], m['n_acc'])
+  ess = eng.trace_ess(10)
+  g = eng.rccl_allgather_stats()
+  assert list(g['counts']) == [1000]
+  np.testing.assert_array_equal(g['sum'], m['sum'])
+  np.testing.assert_array_equal(g['sumsq'], m['sumsq'])
+  np.testing.assert_array_equal(g['n_acc'], m['n_acc'])
+  np.testing.assert_array_equal(g['ess'], ess)
   assert eng.rccl_allreduce_max(2.5) == 2.5
   eng.close()
+
+
+def _ess_ips(x):
+  """scripts/bench_workloads.py's host estimator (FFT autocorrelation)."""
+  n, t = x.shape
+  xc = x - x.mean(axis=1, keepdims=True)
+  f = np.fft.rfft(xc, n=2 * t, axis=1)
+  ac = np.fft.irfft(f * np.conj(f), axis=1)[:, :t]
+  ac /= np.maximum(ac[:, :1], 1e-300)
+  m = (t - 1) // 2
+  pairs = ac[:, 1:2 * m + 1:2] + ac[:, 2:2 * m + 2:2]
+  neg = pairs <= 0
+  first = np.where(neg.any(axis=1), neg.argmax(axis=1), m)
+  keep = np.arange(m)[None, :] < first[:, None]
+  s = np.sum(np.where(keep, pairs, 0.), axis=1)
+  return t / np.maximum(1.0 + 2.0 * s, 1e-12), pairs, first
+
+
+@pytest.mark.parametrize('name,n,t,burn', [('gmm2', 2000, 600, 100),
+                                           ('diag10', 300, 257, 7)])
+def test_device_ess_and_trace_stats_match_host(name, n, t, burn):
+  """pbh_trace_ess (on-device initial positive sequence) equals the host FFT
+  estimator on the same trace within 1e-9 wherever the sequence's stopping
+  pair is not within rounding of zero; pbh_trace_stats equals the host sums
+  of the trace."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec(name)
+  eng = Engine(spec)
+  eng.init_chains(golden_init(name, n))
+  eng.set_rng('philox', seed=17)
+  eng.set_collect(moments=False)
+  eng.alloc_trace(t, 1)
+  eng.run(t, steps_per_launch=100)
+  tr = eng.trace()
+  dev = eng.trace_ess(burn)
+  st = eng.trace_stats(burn)
+  eng.close()
+  x = tr['v_x'][:, burn:]
+  np.testing.assert_allclose(st['sum'], x.sum(1), rtol=1e-12, atol=1e-12)
+  np.testing.assert_allclose(st['sumsq'], (x * x).sum(1), rtol=1e-12, atol=1e-12)
+  assert np.array_equal(st['n_acc'], tr['u'][:, burn:].sum(1))
+  for k in range(x.shape[2]):
+    host, pairs, first = _ess_ips(x[:, :, k])
+    # chains whose decisive pair (the first non-positive one) is within
+    # rounding of 0 may stop one pair apart between the two summations
+    m = pairs.shape[1]
+    dec = np.abs(pairs[np.arange(len(first)), np.minimum(first, m - 1)])
+    clear = dec > 1e-9
+    assert clear.mean() > 0.99
+    rel = np.abs(dev[clear, k] / host[clear] - 1)
+    assert rel.max() < 1e-9, rel.max()
 
 
 @pytest.mark.parametrize('n', [32, 100])
