@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PBH_ABI_VERSION 3
+#define PBH_ABI_VERSION 4
 #define PBH_MAX_DIM 32
 
 #define PBH_OK 0
@@ -55,7 +55,20 @@ enum pbh_proposal_kind {
   PBH_PROP_GAUSS = 1,   /* callable Delta(norm.rvs(loc, scale)) per dim        */
   PBH_PROP_SPHERE = 2,  /* tuple delta, field.py:509-531                      */
   PBH_PROP_UNIFORM = 3, /* list delta, variable.py:625-633                    */
-  PBH_PROP_GIBBS = 4    /* CondCov conditional draw, cond_cov.py:42-65        */
+  PBH_PROP_GIBBS = 4,   /* CondCov conditional draw, cond_cov.py:42-65        */
+  PBH_PROP_VARDELTA = 5 /* per-variable deltas (a Delta of containers, or a
+                           bare scalar Field delta): field.py:266-306,
+                           variable.py:600-640                                */
+};
+/* Per-variable delta modes of PBH_PROP_VARDELTA (Variable.eval_delta,
+ * variable.py:618-633).  Replay streams hold, per variable, the raw uniform
+ * (POLARITY, UNIFORM), the randint value (RANDINT) or nothing (FIXED).     */
+enum pbh_var_delta {
+  PBH_VAR_FIXED = 0,     /* bare scalar: x + delta                             */
+  PBH_VAR_POLARITY = 1,  /* (delta,): +delta if uniform() > 0.5 else -delta    */
+  PBH_VAR_UNIFORM = 2,   /* [delta]: uniform(-delta, delta)                    */
+  PBH_VAR_RANDINT = 3    /* [delta] of an int variable: randint(-delta, delta),
+                            bounds truncated toward zero as NumPy does         */
 };
 enum pbh_rng_mode {
   PBH_RNG_REPLAY = 0,    /* randoms read from a caller-supplied [T][R][N]
@@ -132,6 +145,20 @@ typedef struct pbh_proposal {
    * RF.eval_delta does with the Cholesky factor that RF.set_tran(ndarray)
    * installs (rf.py:210-220, 340-354).  NULL = no tfun.                    */
   const double *tfun;
+  /* VARDELTA: var_mode[d] (enum pbh_var_delta); the steps are delta_vec[d] */
+  const int32_t *var_mode;
+  /* Optional, any MH kind.  var_int[d] = 1: an int variable, whose proposed
+   * value is truncated toward zero (revtype, variable.py:697).  NULL = none. */
+  const int32_t *var_int;
+  /* Optional, any MH kind: bound=True (variable.py:700-739), per dim
+   * bound_on[d]; limits bound_lo[d] <= bound_hi[d] (the vset limits) and
+   * which are exclusive (bound_xlo[d], bound_xhi[d]).  With both limits
+   * closed the proposal is clamped; an exclusive side it crosses returns the
+   * predecessor value (both exclusive: anything outside (lo, hi); one
+   * exclusive: strictly beyond it), the other side is clamped.  NULL = none. */
+  const int32_t *bound_on;
+  const double *bound_lo, *bound_hi;
+  const int32_t *bound_xlo, *bound_xhi;
 } pbh_proposal;
 
 /* CondCov Gibbs tables (replaces CondCov.__init__ + RF.eval_tfun cycling:
@@ -165,6 +192,11 @@ int pbh_set_gibbs(pbh_engine *eng, const pbh_gibbs *gibbs);
  * (sp_utils.py:24-25, App. A-3).                                            */
 int pbh_init_chains(pbh_engine *eng, int64_t n_chains, int64_t chain_offset,
                     const double *init);
+/* Global step index of the first pbh_run step (default 0): the phase of the
+ * CondCov coordinate cycle, which the reference keeps per RF across samplers
+ * (RF.__cond_mod, rf.py:446-452), and the Philox step counter.  Only right
+ * after pbh_init_chains.                                                     */
+int pbh_set_step(pbh_engine *eng, int64_t step);
 int pbh_set_rng(pbh_engine *eng, int32_t mode, uint64_t seed);
 /* Replay stream [n_steps][R][n_chains] (R = d + 1 for MH, 1 for Gibbs),
  * consumed from the next pbh_run step on.                                   */
@@ -276,10 +308,11 @@ int pbh_bool_perm_freq(int device, int64_t rows, int32_t cols,
  * init/final_x [3][n_chains]; rand [n_steps][n_chains] (REPLAY: the standard
  * gauss, or standard_gamma(alpha + n_obs/2) on y_sigma steps, in NumPy's
  * legacy order); trace_x [n_steps][3][n_chains], trace_lp [n_steps][n_chains]
- * (either may be NULL).  rng_mode REPLAY / PHILOX_F64 use the reference's
- * arithmetic; PHILOX uses sufficient statistics.  Host buffers; the chain
- * runs `reps` >= 1 times from init on device-resident inputs after one
- * untimed warm-up, *kernel_ms (may be NULL) = the average kernel time.     */
+ * (either may be NULL: then no device trace is kept).  rng_mode REPLAY /
+ * PHILOX_F64 use the reference's arithmetic; PHILOX uses centred sufficient
+ * statistics.  Host buffers; the chain runs `reps` >= 1 times from init on
+ * device-resident inputs (reps > 1: after one untimed warm-up), *kernel_ms
+ * (may be NULL) = the average kernel time.                                  */
 int pbh_linreg_gibbs(int device, int64_t n_obs, const double *x_obs,
                      const double *y_obs, const double *hyper,
                      const double *vsets, int64_t n_chains,

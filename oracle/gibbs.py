@@ -35,8 +35,11 @@ def condcov_tables(mean, cov, lo, hi):
   return coef, stdv, cdfs
 
 
-def run_gibbs(spec, init, streams):
-  """T coordinate steps for N chains; streams [T, 1, N] of raw uniforms."""
+def run_gibbs(spec, init, streams, step0=0):
+  """T coordinate steps for N chains; streams [T, tsteps, N] of raw uniforms.
+  step0: SP steps the RF already made, i.e. the cycle phase __cond_mod of
+  rf.py:446-452 at which this sampler starts (it persists on the RF across
+  samplers)."""
   prop = spec['proposal']
   d = int(spec['dim'])
   T, _, N = streams.shape
@@ -49,8 +52,9 @@ def run_gibbs(spec, init, streams):
   perm = mvn_perm(d)
   out = {'v_x': np.empty((N, T, d)), 'v_p': np.empty((N, T)),
          'u': np.ones((N, T), np.uint8)}
+  nblk = -(-d // tsteps)
   for c in range(N):
-    cond_mod = 0
+    cond_mod = (int(step0) % nblk) * tsteps
     xc = x[c]
     for t in range(T):
       for j, key in enumerate(range(cond_mod, min(cond_mod + tsteps, d))):

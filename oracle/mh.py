@@ -88,17 +88,56 @@ def _base_delta(spec, draws):
     deltas = (deltas * dl) / rss
     lengths = np.asarray(prop['lengths'])[:, None]
     return deltas * lengths
+  if kind == 'vardelta':
+    # per-variable deltas, Variable.eval_delta (variable.py:600-640); the
+    # stream holds the (redraw-resolved) uniform, or the randint value
+    mode, dl = np.asarray(prop['mode']), np.asarray(prop['delta'])
+    delta = np.empty_like(draws[:d])
+    for k in range(d):
+      if mode[k] == FIXED:
+        delta[k] = dl[k]
+      elif mode[k] == POLARITY:       # delta if uniform() > 0.5 else -delta
+        delta[k] = np.where(draws[k] > 0.5, dl[k], -dl[k])
+      elif mode[k] == UNIFORM:        # uniform(-delta, delta)
+        delta[k] = -dl[k] + (dl[k] - -dl[k]) * draws[k]
+      else:                           # randint(-delta, delta)
+        delta[k] = draws[k]
+    return delta
   raise ValueError(kind)
 
 
+# per-variable delta modes of the 'vardelta' proposal (variable.py:600-640)
+FIXED, POLARITY, UNIFORM, RANDINT = 0, 1, 2, 3
+
+
 def apply_delta(spec, x, delta):
-  """variable.py:693-697: x + delta, or ufun[1](ufun[0](x) + delta)."""
+  """variable.py:693-739 per chain (scalar values): x + delta, or
+  ufun[1](ufun[0](x) + delta); revtype to int for int variables; then, with
+  bound=True, a clamp to closed limits, or for an exclusive limit the
+  predecessor value (the scalar branch, variable.py:715-728)."""
+  prop = spec['proposal']
+  vint = prop.get('vint')
+  bnd = prop.get('bound')
   out = np.empty_like(x)
   for k in range(int(spec['dim'])):
     if spec['ufun'][k]:
-      out[k] = np.exp(np.log(x[k]) + delta[k])
+      v = np.exp(np.log(x[k]) + delta[k])
     else:
-      out[k] = x[k] + delta[k]
+      v = x[k] + delta[k]
+    if vint is not None and vint[k]:
+      v = np.trunc(v)                 # vtypes.py:156-166 int(v)
+    if bnd is not None and bnd['on'][k]:
+      lo, hi = bnd['lo'][k], bnd['hi'][k]
+      xl, xh = bnd['xlo'][k], bnd['xhi'][k]
+      if not xl and not xh:
+        v = np.maximum(lo, np.minimum(hi, v))
+      elif xl and xh:
+        v = np.where((v > lo) & (v < hi), v, x[k])
+      elif xl:
+        v = np.where(v < lo, x[k], np.minimum(hi, v))
+      else:
+        v = np.where(v > hi, x[k], np.maximum(lo, v))
+    out[k] = v
   return out
 
 

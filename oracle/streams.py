@@ -36,14 +36,17 @@ def gibbs_coords(d, tsteps, n_steps):
   return out
 
 
-def legacy_streams(spec, seeds, n_steps):
-  """Per-chain np.random.RandomState(seed) streams, shape [T, R, N]."""
+def legacy_streams(spec, seeds, n_steps, states=None):
+  """Per-chain np.random.RandomState(seed) streams, shape [T, R, N].
+  states: a list that receives each chain's RandomState after the draws."""
   seeds = np.asarray(seeds).reshape(-1)
   n, d, r = seeds.size, int(spec['dim']), stream_width(spec)
   kind = spec['proposal']['kind']
   out = np.empty((n_steps, r, n), dtype=np.float64)
   for c, seed in enumerate(seeds):
     rs = np.random.RandomState(int(seed))
+    if states is not None:
+      states.append(rs)
     col = out[:, :, c]
     if kind == 'gibbs':
       col[:] = np.nan
@@ -55,7 +58,28 @@ def legacy_streams(spec, seeds, n_steps):
         # d separate norm.rvs calls == one standard_normal(d): the polar
         # method's cached second deviate persists across calls either way.
         col[t, :d] = rs.standard_normal(d)
+      elif kind in ('uniform', 'vardelta'):
+        _per_variable_draws(rs, spec['proposal'], d, col[t])
       else:
         col[t, :d] = rs.random_sample(d)
       col[t, d] = rs.random_sample()
   return out
+
+
+def _per_variable_draws(rs, prop, d, row):
+  """Field.eval_delta draws every variable's delta in key order
+  (field.py:477-483, variable.py:618-633): tuple -> uniform() for the
+  polarity, list -> uniform(-d, d) or, for an int variable, randint(-d, d),
+  bare scalar -> nothing.  Each value comes back wrapped in the variable's
+  Delta namedtuple, so apply_delta's `delta or self._delta`
+  (variable.py:660) never redraws, not even a zero.  row[k] keeps the raw
+  uniform, or the randint value; NaN for a fixed step."""
+  from oracle.mh import FIXED, RANDINT
+  mode = np.full(d, 2) if prop['kind'] == 'uniform' else np.asarray(prop['mode'])
+  dl = np.asarray(prop['delta'], np.float64)
+  row[:d] = np.nan
+  for k in range(d):
+    if mode[k] == RANDINT:
+      row[k] = rs.randint(-dl[k], dl[k])
+    elif mode[k] != FIXED:
+      row[k] = rs.random_sample()

@@ -65,9 +65,11 @@ def spec_metrohast_norm1d(params):
                 'scale': 1},
                {'kind': 'sphere', 'delta': 0.005 * rss, 'lengths': lengths},
                tran={'kind': 'const', 'value': 1.0, 'sym': False},
+               # tuple vsets (40, 60), (5, 20.): both limits exclusive
+               # (variable.py:178-183, 360-366)
                prior={'lo': np.array([40., 5.]), 'hi': np.array([60., 20.]),
-                      'lo_incl': np.array([1, 1], np.int32),
-                      'hi_incl': np.array([1, 1], np.int32),
+                      'lo_incl': np.array([0, 0], np.int32),
+                      'hi_incl': np.array([0, 0], np.int32),
                       'logp': float(prior_logp)},
                ufun=[0, 1])
 
@@ -189,12 +191,88 @@ def spec_covrw5(params):
                tran={'kind': 'const', 'value': 1.0, 'sym': False})
 
 
+# ----------------------------------------------------------------------------
+# Delta forms (tests/mcmc_examples.py DELTA_WORKLOADS): per-variable modes
+# FIXED / POLARITY / UNIFORM / RANDINT (oracle.mh), int truncation and the
+# bound=True clamp / bounce of variable.py:700-739.
+# ----------------------------------------------------------------------------
+def _bound(lo, hi, xlo, xhi, on=None):
+  d = len(lo)
+  return {'lo': np.asarray(lo, np.float64), 'hi': np.asarray(hi, np.float64),
+          'xlo': np.asarray(xlo, np.int32), 'xhi': np.asarray(xhi, np.int32),
+          'on': np.ones(d, np.int32) if on is None else np.asarray(on, np.int32)}
+
+
+def _diag(mu, sigma):
+  return {'kind': 'diag_gauss', 'mu': np.asarray(mu, np.float64),
+          'sigma': np.asarray(sigma, np.float64)}
+
+
+# x [(-1,), 1], y [-1, (1,)], z [0, 2] (tests/mcmc_examples.py _three_vsets)
+_B3 = _bound([-1., -1., 0.], [1., 1., 2.], [1, 0, 0], [0, 1, 0])
+_T3 = _diag([-0.8, 0.8, 1.9], [0.5, 0.5, 0.6])
+
+
+def spec_bound_sphere2(params):
+  """omc_rw_circle.py:16-22: tuple vsets = both limits exclusive
+  (variable.py:178-183), unscaled spherical delta, bound=True bounces."""
+  prop = {'kind': 'sphere', 'delta': float(params['step']),
+          'lengths': np.ones(2), 'bound': _bound([-1., -1.], [1., 1.],
+                                                 [1, 1], [1, 1])}
+  return _spec(2, ['x', 'y'], _diag([0.7, -0.6], [0.4, 0.5]), prop)
+
+
+def spec_bound_list3(params):
+  """set_delta([0.2], {'z': 0.15}, scale=True, bound=True): x, y uniform
+  +-0.2 * length 2, z +-0.15 unscaled (field.py:276-306)."""
+  prop = {'kind': 'uniform', 'delta': np.array([0.2 * 2., 0.2 * 2., 0.15]),
+          'bound': _B3}
+  return _spec(3, ['x', 'y', 'z'], _T3, prop)
+
+
+def spec_pervar3(params):
+  """Delta(x=(0.25,), y=[0.3], z=0.05), scale=True: only the bare scalar is
+  scaled by its length (variable.py:637-639)."""
+  prop = {'kind': 'vardelta', 'mode': np.array([1, 2, 0], np.int32),
+          'delta': np.array([0.25, 0.3, 0.05 * 2.]), 'bound': _B3}
+  return _spec(3, ['x', 'y', 'z'], _T3, prop)
+
+
+def spec_dict3(params):
+  """A dict delta leaves every value unchanged (tests/mcmc_examples.py dict3):
+  fixed zero steps, no bound (apply_delta returns before bounding)."""
+  prop = {'kind': 'vardelta', 'mode': np.zeros(3, np.int32),
+          'delta': np.zeros(3)}
+  return _spec(3, ['x', 'y', 'z'], _T3, prop)
+
+
+def spec_fixed2(params):
+  """set_delta(0.02, {'y': -0.03}, scale=True, bound=True) on [-1, 1]^2."""
+  prop = {'kind': 'vardelta', 'mode': np.zeros(2, np.int32),
+          'delta': np.array([0.02 * 2., -0.03]),
+          'bound': _bound([-1., -1.], [1., 1.], [0, 0], [0, 0])}
+  return _spec(2, ['x', 'y'], _diag([0.3, -0.2], [0.5, 0.4]), prop)
+
+
+def spec_randint2(params):
+  """Delta(n=[3], x=[0.5]), bound=True: n int in range(0, 21) draws
+  randint(-3, 3) and clamps to [0, 20]; x's tuple vset (-inf, inf) bounces
+  only non-finite values."""
+  prop = {'kind': 'vardelta', 'mode': np.array([3, 2], np.int32),
+          'delta': np.array([3., 0.5]), 'vint': np.array([1, 0], np.int32),
+          'bound': _bound([0., -np.inf], [20., np.inf], [0, 1], [0, 1])}
+  return _spec(2, ['n', 'x'], _diag([12., 0.], [3., 1.]), prop)
+
+
 INITS = {
     'metrohast_norm1d': [50., 12.5], 'mcmc_prob2': [0.], 'mcmc_prob3': [5.],
     'mcmc_prob4a': [0., 1.], 'mcmc_prob4b': [5., 5.], 'mcmc_prob6': [0., 1.],
     'gibbs_norm2d': [0., 1.], 'diag10': [0.] * 10, 'gibbs8': [0.] * 8,
     'gibbs_sweep2': [0., 0.],
     'gmm2': [0., 0.], 'covrw2': [0., 0.], 'covrw5': [0.] * 5,
+    'bound_sphere2': [0., 0.], 'bound_list3': [0., 0., 1.],
+    'pervar3': [0., 0., 1.], 'dict3': [0.1, 0.2, 1.], 'fixed2': [0., 0.],
+    'randint2': [0., 0.],
 }
 
 WORKLOADS = {
@@ -205,7 +283,14 @@ WORKLOADS = {
     'gibbs8': spec_gibbs8, 'gmm2': spec_gmm2,
     'gibbs_sweep2': spec_gibbs_sweep2,
     'covrw2': spec_covrw2, 'covrw5': spec_covrw5,
+    'bound_sphere2': spec_bound_sphere2, 'bound_list3': spec_bound_list3,
+    'pervar3': spec_pervar3, 'dict3': spec_dict3, 'fixed2': spec_fixed2,
+    'randint2': spec_randint2,
 }
+
+# consecutive samplers on one process (tests/mcmc_examples.py SEGMENTED)
+SEGMENTED = {'gibbs_norm2d_seg': 'gibbs_norm2d',
+             'gibbs_linreg_seg': 'gibbs_linreg'}
 
 
 def golden_params(g):

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PBHIP_LIB', os.path.join(_HERE, 'libpbhip.so'))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_DIM = 32
 
 # enums (pbhip.h)
@@ -20,7 +20,9 @@ TARGET = {'diag_gauss': 1, 'norm_iid': 2, 'gmm': 3, 'norm_pdf': 4,
 PSCALE = {'log': 0, 'lin': 1}
 SCORES = {'hastings': 1, 'metropolis': 2, 'gibbs': 3}
 TRAN = {'const': 1, 'gauss_pdf': 2}
-PROPOSAL = {'gauss': 1, 'sphere': 2, 'uniform': 3, 'gibbs': 4}
+PROPOSAL = {'gauss': 1, 'sphere': 2, 'uniform': 3, 'gibbs': 4, 'vardelta': 5}
+# enum pbh_var_delta
+VAR_FIXED, VAR_POLARITY, VAR_UNIFORM, VAR_RANDINT = 0, 1, 2, 3
 RNG = {'replay': 0, 'philox': 1, 'philox_f64': 2, 'xoshiro': 3,
        'philox_fp32': 4}
 COLLECT_MOMENTS = 1
@@ -54,7 +56,9 @@ class PbhProposal(ctypes.Structure):
   _fields_ = [
       ('kind', ctypes.c_int32), ('loc', _dp), ('scale', _dp),
       ('order', _ip), ('delta', ctypes.c_double), ('lengths', _dp),
-      ('delta_vec', _dp), ('tfun', _dp),
+      ('delta_vec', _dp), ('tfun', _dp), ('var_mode', _ip), ('var_int', _ip),
+      ('bound_on', _ip), ('bound_lo', _dp), ('bound_hi', _dp),
+      ('bound_xlo', _ip), ('bound_xhi', _ip),
   ]
 
 
@@ -76,6 +80,7 @@ SIGNATURES = {
     'pbh_set_gibbs': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PbhGibbs)]),
     'pbh_init_chains': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                        ctypes.c_int64, _dp]),
+    'pbh_set_step': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     'pbh_set_rng': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
                                    ctypes.c_uint64]),
     'pbh_upload_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _dp]),

@@ -28,6 +28,10 @@ struct KArgs {
   double sdelta;
   const double *ptf;  // covariance RW: delta' = ptf[d][d] . delta (rf.py:340-354)
   int32_t has_tfun;
+  uint64_t vmode;     // VARDELTA: enum pbh_var_delta, 2 bits per dim
+  uint32_t vint;      // bitmask: int variable (proposal truncated)
+  uint32_t bnd_on, bnd_xlo, bnd_xhi;  // bound=True: on / exclusive lo / hi
+  const double *blo, *bhi;            // bound limits [d]
   // ---- gibbs ----
   const double *gmean, *gcoef, *gstdv, *gcdf;
   int32_t tsteps;
@@ -121,6 +125,9 @@ struct LegacyArgs {
   double *out;          // replay rows [n_steps][R][n]
   int64_t n, n_steps, step0;
   int32_t d, R, gibbs, normal;
+  int32_t vardelta;     // VARDELTA: per-dim modes vmode, steps vdelta [d]
+  uint64_t vmode;
+  const double *vdelta;
 };
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
@@ -141,11 +148,11 @@ hipError_t launch_check_accept(int64_t n, const double *lp, const double *lpp,
 
 // user-conditional Gibbs of the gibbs_linreg model (pbh_linreg.hip).
 // hyper: p0, m0, p1, m1, alpha_post, beta, sxx, prior[3], logC;
-// stats: Sx, Sy, Sxy, Syy (PHILOX's fast form).
+// stats: xbar, ybar, Cxx, Cxy, Cyy (centred; PHILOX's fast form).
 struct LinregArgs {
   const double *x_obs, *y_obs;
   int64_t n_obs;
-  double hyper[11], stats[4], bounds[6];  // bounds: (lo, hi) per parameter
+  double hyper[11], stats[5], bounds[6];  // bounds: (lo, hi) per parameter
   double *state, *lp_state;
   const double *rand;
   double *tx, *tp;

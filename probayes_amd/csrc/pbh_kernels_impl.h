@@ -350,6 +350,37 @@ __device__ __forceinline__ bool score(const KArgs &a, const double (&x)[D],
 }
 
 // ---------------------------------------------------------------------------
+// Per-variable delta helpers (variable.py:618-739)
+// ---------------------------------------------------------------------------
+// np.minimum / np.maximum: a NaN operand propagates
+__device__ __forceinline__ double np_minimum(double a, double b) {
+  return (a != a || b != b) ? a + b : (a < b ? a : b);
+}
+__device__ __forceinline__ double np_maximum(double a, double b) {
+  return (a != a || b != b) ? a + b : (a > b ? a : b);
+}
+
+// bound=True on one scalar value (variable.py:711-728): closed limits clamp;
+// both exclusive: outside (lo, hi) returns the predecessor xo; one exclusive
+// side: strictly beyond it returns xo, the other side clamps.
+__device__ __forceinline__ double bound_value(double v, double xo, double lo,
+                                              double hi, bool xl, bool xh) {
+  if (!xl && !xh) return np_maximum(lo, np_minimum(hi, v));
+  if (xl && xh) return (v > lo && v < hi) ? v : xo;
+  if (xl) return v < lo ? xo : np_minimum(hi, v);
+  return v > hi ? xo : np_maximum(lo, v);
+}
+
+// randint(-d0, d0) in the production modes from one 53-bit uniform: NumPy
+// truncates both bounds toward zero; the value is lo + floor(u * span),
+// uniform over [lo, hi) to within span * 2^-53.
+__device__ __forceinline__ double randint_u(double u, double d0) {
+  const double lo = trunc(-d0), span = trunc(d0) - lo;
+  const double k = floor(u * span);
+  return lo + (k < span - 1. ? k : span - 1.);
+}
+
+// ---------------------------------------------------------------------------
 // MH kernel: n_steps fused chain-steps, one chain per lane
 // ---------------------------------------------------------------------------
 template <int D, int RNG, int TGT, int PROP>
@@ -490,6 +521,21 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
           const double d0 = cld(a.pdel, k);
           dl[k] = -d0 + (d0 - -d0) * r[k];
         }
+      } else if (prop == PBH_PROP_VARDELTA) {
+        // per-variable deltas (variable.py:618-640), modes 2 bits per dim
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double d0 = cld(a.pdel, k);
+          const int md = (int)((a.vmode >> (2 * k)) & 3u);
+          if (md == PBH_VAR_FIXED)
+            dl[k] = d0;
+          else if (md == PBH_VAR_POLARITY)
+            dl[k] = r[k] > 0.5 ? d0 : -d0;
+          else if (md == PBH_VAR_UNIFORM)
+            dl[k] = -d0 + (d0 - -d0) * r[k];
+          else   // replay streams carry the randint value itself
+            dl[k] = RNG == PBH_RNG_REPLAY ? r[k] : randint_u(r[k], d0);
+        }
       } else {
         // spherical tuple delta (field.py:509-531)
         const double d0 = a.sdelta;
@@ -510,6 +556,15 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         xp[k] = ((a.ufun >> k) & 1u)
                     ? (FAST ? fast_exp(fast_log(x[k]) + dl[k]) : exp(log(x[k]) + dl[k]))
                     : x[k] + dl[k];
+      if (a.vint | a.bnd_on) {   // wave-uniform: int variables, bound=True
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          if ((a.vint >> k) & 1u) xp[k] = trunc(xp[k]);
+          if ((a.bnd_on >> k) & 1u)
+            xp[k] = bound_value(xp[k], x[k], cld(a.blo, k), cld(a.bhi, k),
+                                (a.bnd_xlo >> k) & 1u, (a.bnd_xhi >> k) & 1u);
+        }
+      }
     }
     // ---- density, score, accept ----
     const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
@@ -2132,7 +2187,7 @@ void launch_mh_pair(const KArgs &a, hipStream_t st) {
 // Gaussian delta, no ufun / prior, symmetric tran or metropolis, debug off.
 inline bool pair_form(const KArgs &a) {
   return a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS &&
-         a.ufun == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
+         a.ufun == 0 && a.vint == 0 && a.bnd_on == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
          a.d * a.n * 8 < (int64_t(1) << 32) &&   // 32-bit trace byte offsets
          (a.scores == PBH_SCORES_METROPOLIS ||
           (a.scores == PBH_SCORES_HASTINGS && a.tran_sym &&
@@ -2143,7 +2198,7 @@ inline bool pair_form(const KArgs &a) {
 // ufun / prior / debug records.
 inline bool gmm_pair_form(const KArgs &a) {
   return a.rng == PBH_RNG_PHILOX && a.simple_acc && a.pair_ok && a.ufun == 0 &&
-         !a.has_prior && !a.debug && !a.has_tfun &&
+         a.vint == 0 && a.bnd_on == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
          a.d * a.n * 8 < (int64_t(1) << 32);   // 32-bit trace byte offsets
 }
 

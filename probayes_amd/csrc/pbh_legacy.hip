@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "pbh_kernels.h"
+#include "pbhip.h"
 
 namespace pbh {
 namespace {
@@ -126,6 +127,23 @@ __device__ __forceinline__ double legacy_gauss(Mt &m, double &gauss, int &has) {
   return f * x2;
 }
 
+// RandomState.randint(-d0, d0) (mtrand.pyx randint -> _rand_int64 with
+// use_masked=True): bounds truncated toward zero, rng = hi - 1 - lo, then
+// words & mask (the smallest all-ones >= rng) until <= rng
+// (distributions.c buffered_bounded_masked_uint32).
+__device__ __forceinline__ double legacy_randint(Mt &m, double d0) {
+  const int64_t lo = (int64_t)trunc(-d0), hi = (int64_t)trunc(d0);
+  const uint32_t rng = (uint32_t)(hi - 1 - lo);
+  if (rng == 0) return (double)lo;
+  uint32_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+  mask |= mask >> 8; mask |= mask >> 16;
+  uint32_t v;
+  while ((v = (m.next32() & mask)) > rng) {
+  }
+  return (double)(lo + (int64_t)v);
+}
+
 __global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.n) return;
@@ -142,6 +160,20 @@ __global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
       const int cnt = (cm + a.R < a.d ? cm + a.R : a.d) - cm;
       for (int j = 0; j < a.R; ++j)
         row[(int64_t)j * a.n] = j < cnt ? m.next_double() : __builtin_nan("");
+      continue;
+    }
+    if (a.vardelta) {
+      // Field.eval_delta draws per variable in key order (variable.py:618-633)
+      for (int j = 0; j < a.d; ++j) {
+        const int md = (int)((a.vmode >> (2 * j)) & 3u);
+        double v = __builtin_nan("");
+        if (md == PBH_VAR_RANDINT)
+          v = legacy_randint(m, a.vdelta[j]);
+        else if (md != PBH_VAR_FIXED)
+          v = m.next_double();
+        row[(int64_t)j * a.n] = v;
+      }
+      row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
       continue;
     }
     for (int j = 0; j < a.d; ++j) {

@@ -14,8 +14,12 @@
 //   EXACT (REPLAY, PHILOX_F64): the reference's operations -- numpy's pairwise
 //     sums over the observations, true IEEE divisions, scipy's logpdf -- so a
 //     REPLAY run reproduces the reference chain from its standard draws;
-//   FAST (PHILOX): the sums come from the sufficient statistics Sx, Sy, Sxx,
-//     Sxy, Syy (O(1) per step instead of O(n)); same conditional law.
+//   FAST (PHILOX): the sums come from CENTRED sufficient statistics (O(1) per
+//     step instead of O(n)); same conditional law.  With xbar, ybar and the
+//     centred Cxx, Cxy, Cyy (host, long double, two passes):
+//       sum (y - b0 - b1 x)^2 = Cyy + b1 (b1 Cxx - 2 Cxy) + n (ybar - b0 - b1 xbar)^2,
+//       sum (y - b1 x) = n (ybar - b1 xbar),  sum x (y - b0) = Cxy + n xbar (ybar - b0),
+//     free of the cancellation of raw moments when x or y carry a large offset.
 // Draws: REPLAY reads the standard gauss / standard_gamma(a + n/2) of each step
 // from rand[T][N]; PHILOX modes draw fp64 Box-Muller normals (libm in
 // PHILOX_F64, LDS tables in PHILOX) and Marsaglia-Tsang gammas from
@@ -49,7 +53,7 @@ struct LinregK {
   // sxx = np.sum(x**2) (host), prior[3], logC, and the sufficient statistics
   // Sx, Sy, Sxy, Syy (FAST only)
   double p0, m0, p1, m1, alpha, beta, sxx, pri0, pri1, pri2, logC;
-  double sx, sy, sxy, syy;
+  double xbar, ybar, cxx, cxy, cyy;     // centred statistics (FAST only)
   double lo0, hi0, lo1, hi1, lo2, hi2;  // closed vsets of the root priors
   double *state;          // [3][n] beta_0, beta_1, y_sigma (in/out)
   double *lp_state;       // [n] (out)
@@ -108,6 +112,13 @@ __device__ __forceinline__ double mt_gamma(const LinregK &a, const BMTables *tb,
   return out;
 }
 
+// sum_j (y_j - b0 - b1 x_j)^2 from the centred statistics
+__device__ __forceinline__ double fast_ss(const LinregK &a, double nd, double b0,
+                                          double b1) {
+  const double r = a.ybar - b0 - b1 * a.xbar;
+  return __builtin_fma(nd * r, r, __builtin_fma(b1, __builtin_fma(b1, a.cxx, -2.0 * a.cxy), a.cyy));
+}
+
 template <bool EXACT>
 __global__ void __launch_bounds__(kBlock)
 linreg_gibbs_kernel(LinregK a) {
@@ -161,8 +172,7 @@ linreg_gibbs_kernel(LinregK a) {
           return r * r;
         }, a.n_obs);
       } else {
-        ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx - 2.0 * b0 * a.sy -
-             2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
+        ss = fast_ss(a, nd, b0, b1);
       }
       const double cb = a.beta + 0.5 * ss;
       sg = 1.0 / sqrt((1.0 / cb) * z);
@@ -175,13 +185,14 @@ linreg_gibbs_kernel(LinregK a) {
       if (key == 0) {
         const double v = 1.0 / (a.p0 + nd * yp);
         const double s = EXACT ? np_pairwise([&](int64_t j) {
-          return ys_obs[j] - b1 * xs[j]; }, a.n_obs) : a.sy - b1 * a.sx;
+          return ys_obs[j] - b1 * xs[j]; }, a.n_obs) : nd * (a.ybar - b1 * a.xbar);
         const double m = (a.p0 * a.m0 + yp * s) * v;
         b0 = m + sqrt(v) * z;
       } else {
         const double v = 1.0 / (a.p1 + yp * a.sxx);
         const double s = EXACT ? np_pairwise([&](int64_t j) {
-          return xs[j] * (ys_obs[j] - b0); }, a.n_obs) : a.sxy - b0 * a.sx;
+          return xs[j] * (ys_obs[j] - b0); }, a.n_obs)
+                               : __builtin_fma(nd * a.xbar, a.ybar - b0, a.cxy);
         const double m = (a.p1 * a.m1 + yp * s) * v;
         b1 = m + sqrt(v) * z;
       }
@@ -193,9 +204,7 @@ linreg_gibbs_kernel(LinregK a) {
         return lr_norm_logpdf(ys_obs[j], b0 + b1 * xs[j], sg, lsg, a.logC);
       }, a.n_obs);
     } else {
-      const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx -
-                        2.0 * b0 * a.sy - 2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
-      lp = -0.5 * ss / (sg * sg) - nd * (a.logC + lsg);
+      lp = -0.5 * fast_ss(a, nd, b0, b1) / (sg * sg) - nd * (a.logC + lsg);
     }
     // uniform_prob (rv_utils.py:30-38): -log L inside the vset, else
     // NEARLY_NEGATIVE_INF; added one parameter at a time
@@ -203,11 +212,13 @@ linreg_gibbs_kernel(LinregK a) {
     const double q1 = (b1 >= a.lo1 && b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
     const double q2 = (sg >= a.lo2 && sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
     lp = ((lp + q0) + q1) + q2;
-    double *tx = a.tx + t * 3 * n;
-    __builtin_nontemporal_store(b0, tx + c);
-    __builtin_nontemporal_store(b1, tx + n + c);
-    __builtin_nontemporal_store(sg, tx + 2 * n + c);
-    __builtin_nontemporal_store(lp, a.tp + t * n + c);
+    if (a.tx) {   // uniform: the trace buffers are optional
+      double *tx = a.tx + t * 3 * n;
+      __builtin_nontemporal_store(b0, tx + c);
+      __builtin_nontemporal_store(b1, tx + n + c);
+      __builtin_nontemporal_store(sg, tx + 2 * n + c);
+    }
+    if (a.tp) __builtin_nontemporal_store(lp, a.tp + t * n + c);
   }
   a.state[c] = b0;
   a.state[n + c] = b1;
@@ -221,28 +232,24 @@ __device__ __forceinline__ void fast_step(const LinregK &a, int key, double z,
                                           double nd, double &b0, double &b1,
                                           double &sg, double &lp) {
   if (key == 2) {
-    const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx - 2.0 * b0 * a.sy -
-                      2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
-    const double cb = a.beta + 0.5 * ss;
+    const double cb = a.beta + 0.5 * fast_ss(a, nd, b0, b1);
     sg = 1.0 / sqrt((1.0 / cb) * z);
   } else {
     const double yp = 1.0 / (sg * sg);
     if (key == 0) {
       const double v = 1.0 / (a.p0 + nd * yp);
-      const double s = a.sy - b1 * a.sx;
+      const double s = nd * (a.ybar - b1 * a.xbar);
       const double m = (a.p0 * a.m0 + yp * s) * v;
       b0 = m + sqrt(v) * z;
     } else {
       const double v = 1.0 / (a.p1 + yp * a.sxx);
-      const double s = a.sxy - b0 * a.sx;
+      const double s = __builtin_fma(nd * a.xbar, a.ybar - b0, a.cxy);
       const double m = (a.p1 * a.m1 + yp * s) * v;
       b1 = m + sqrt(v) * z;
     }
   }
   const double lsg = fast_log(sg);
-  const double ss = a.syy + nd * b0 * b0 + b1 * b1 * a.sxx -
-                    2.0 * b0 * a.sy - 2.0 * b1 * a.sxy + 2.0 * b0 * b1 * a.sx;
-  lp = -0.5 * ss / (sg * sg) - nd * (a.logC + lsg);
+  lp = -0.5 * fast_ss(a, nd, b0, b1) / (sg * sg) - nd * (a.logC + lsg);
   const double q0 = (b0 >= a.lo0 && b0 <= a.hi0) ? a.pri0 : kNearlyNegInf;
   const double q1 = (b1 >= a.lo1 && b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
   const double q2 = (sg >= a.lo2 && sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
@@ -336,13 +343,13 @@ linreg_pair_kernel(LinregK a) {
     const double z = key == 0 ? z0 : (key == 1 ? z1 : g);
     fast_step(a, key, z, nd, b0, b1, sg, lp);
     if (live) {
-      double *tx = a.tx + t * 3 * n;
-      if (!hi) {
+      if (!hi && a.tx) {
+        double *tx = a.tx + t * 3 * n;
         __builtin_nontemporal_store(b0, tx + c);
         __builtin_nontemporal_store(b1, tx + n + c);
-      } else {
-        __builtin_nontemporal_store(sg, tx + 2 * n + c);
-        __builtin_nontemporal_store(lp, a.tp + t * n + c);
+      } else if (hi) {
+        if (a.tx) __builtin_nontemporal_store(sg, a.tx + t * 3 * n + 2 * n + c);
+        if (a.tp) __builtin_nontemporal_store(lp, a.tp + t * n + c);
       }
     }
   }
@@ -370,7 +377,8 @@ hipError_t launch_linreg_gibbs(const LinregArgs &h, hipStream_t s) {
   a.logC = h.hyper[10];
   a.lo0 = h.bounds[0]; a.hi0 = h.bounds[1]; a.lo1 = h.bounds[2];
   a.hi1 = h.bounds[3]; a.lo2 = h.bounds[4]; a.hi2 = h.bounds[5];
-  a.sx = h.stats[0]; a.sy = h.stats[1]; a.sxy = h.stats[2]; a.syy = h.stats[3];
+  a.xbar = h.stats[0]; a.ybar = h.stats[1]; a.cxx = h.stats[2];
+  a.cxy = h.stats[3]; a.cyy = h.stats[4];
   a.state = h.state; a.lp_state = h.lp_state; a.rand = h.rand;
   a.tx = h.tx; a.tp = h.tp;
   a.n = h.n; a.chain_offset = h.chain_offset; a.n_steps = h.n_steps;

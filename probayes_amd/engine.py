@@ -169,6 +169,17 @@ class Engine:
       q.lengths = _dp(arr(p['lengths']))
     elif p['kind'] == 'uniform':
       q.delta_vec = _dp(arr(p['delta']))
+    elif p['kind'] == 'vardelta':
+      q.delta_vec = _dp(arr(p['delta']))
+      q.var_mode = _ip(arr(p['mode'], _i32))
+    if p.get('vint') is not None:
+      q.var_int = _ip(arr(p['vint'], _i32))
+    b = p.get('bound')
+    if b is not None:
+      q.bound_on = _ip(arr(b['on'], _i32))
+      q.bound_lo, q.bound_hi = _dp(arr(b['lo'])), _dp(arr(b['hi']))
+      q.bound_xlo = _ip(arr(b['xlo'], _i32))
+      q.bound_xhi = _ip(arr(b['xhi'], _i32))
     if p.get('tfun') is not None:
       q.tfun = _dp(arr(np.ascontiguousarray(p['tfun'], np.float64)))
     _lib.call('pbh_set_proposal', self._h, _c.byref(q))
@@ -190,6 +201,11 @@ class Engine:
     _lib.call('pbh_init_chains', self._h, _c.c_int64(self.n),
               _c.c_int64(int(chain_offset)), _dp(init))
     self.chain_offset = int(chain_offset)
+
+  def set_step(self, step):
+    """Global step index of the first run step (the CondCov cycle phase,
+    rf.py:446-452); right after init_chains."""
+    _lib.call('pbh_set_step', self._h, _c.c_int64(int(step)))
 
   def set_rng(self, mode='philox', seed=0):
     _lib.call('pbh_set_rng', self._h, _lib.RNG[mode],

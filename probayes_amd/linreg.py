@@ -106,6 +106,9 @@ def run(x_obs, y_obs, init, n_steps, hyper=(0., 1., 0., 1., 1., 1.),
   if tx is not None:
     out['v_x'] = np.transpose(tx, (2, 0, 1)).copy()
     out['v_p'] = tp.T.copy()
+  elif trace:   # T == 0: empty traces, as the MH path returns
+    out['v_x'] = np.empty((n, 0, 3))
+    out['v_p'] = np.empty((n, 0))
   return out
 
 

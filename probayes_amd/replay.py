@@ -15,14 +15,27 @@ standard normals z, uniforms as the raw random_sample double.
 import numpy as np
 
 
-def _fill(rs, kind, d, tsteps, n_coords, col):
-  """Fills col [T, R] from RandomState rs."""
+def _fill(rs, kind, d, tsteps, n_coords, col, var=None):
+  """Fills col [T, R] from RandomState rs.  var = (modes, steps) of a
+  VARDELTA proposal: per variable in key order a randint value, a raw
+  uniform, or nothing for a fixed step (variable.py:618-633)."""
   T = col.shape[0]
   if kind == 'gibbs':
     col[:] = np.nan
     for t in range(T):
       m = n_coords[t]
       col[t, :m] = rs.random_sample(m)
+    return
+  if kind == 'vardelta':
+    modes, steps = var
+    col[:, :d] = np.nan
+    for t in range(T):
+      for k in range(d):
+        if modes[k] == 3:
+          col[t, k] = rs.randint(-steps[k], steps[k])
+        elif modes[k] != 0:
+          col[t, k] = rs.random_sample()
+      col[t, d] = rs.random_sample()
     return
   for t in range(T):
     if kind == 'gauss':
@@ -71,16 +84,19 @@ def legacy_streams(spec, n_steps, seeds=None, step0=0):
   coords = gibbs_coords_per_step(d, tsteps, n_steps, step0) \
       if kind == 'gibbs' else None
   r = stream_width(spec)
+  var = (np.asarray(spec['proposal']['mode']),
+         np.asarray(spec['proposal']['delta'], np.float64)) \
+      if kind == 'vardelta' else None
   if seeds is None:
     out = np.empty((n_steps, r, 1))
     col = np.empty((n_steps, r))
-    _fill(np.random.mtrand._rand, kind, d, tsteps, coords, col)
+    _fill(np.random.mtrand._rand, kind, d, tsteps, coords, col, var)
     out[:, :, 0] = col
     return out
   seeds = np.asarray(seeds).reshape(-1)
   out = np.empty((n_steps, r, seeds.size))
   col = np.empty((n_steps, r))
   for c, s in enumerate(seeds):
-    _fill(np.random.RandomState(int(s)), kind, d, tsteps, coords, col)
+    _fill(np.random.RandomState(int(s)), kind, d, tsteps, coords, col, var)
     out[:, :, c] = col
   return out

@@ -17,21 +17,53 @@ class RV:
   """A random variable (rv.py:28)."""
 
   def __init__(self, name, vtype=float, vset=None, pscale=None, *args, **kwds):
-    if vtype not in (float, np.float64, 'float'):
+    if vtype in (float, np.float64, 'float'):
+      vtype = float
+    elif vtype in (int, np.int64, 'int'):
+      vtype = int
+    else:
       raise NotImplementedError(
-          'RV {}: only float variables are on the GPU MH path'.format(name))
+          'RV {}: only float and int variables are on the GPU MH path'
+          .format(name))
     self.name = str(name)
-    self.vtype = float
+    self.vtype = vtype
     self.vset = vset
     self.pscale = pscale
     self.ufun = None
     self._log_ufun = False
-    self._parse_vset(vset)
+    if vtype is int:
+      self._parse_int_vset(vset)
+    else:
+      self._parse_vset(vset)
+
+  def _parse_int_vset(self, vset):
+    """Non-float value sets (variable.py:169-205, 258-261, 322-329): a
+    list / set / range / array of values; vlims = (min, max), length = the
+    number of values, both limits inclusive."""
+    if vset is None:
+      vset = [0, 1]                          # DEFAULT_VSETS[int]
+    if isinstance(vset, tuple):
+      raise NotImplementedError('RV {}: a tuple vset makes the variable a '
+                                'float'.format(self.name))
+    vals = sorted(int(v) for v in vset)
+    if not vals:
+      raise ValueError('RV {}: empty vset'.format(self.name))
+    self.vset = vals
+    self.vlims = np.array([float(vals[0]), float(vals[-1])])
+    self.lo_incl = self.hi_incl = True
+    self._int_len = len(vals)
 
   def _parse_vset(self, vset):
+    """Float limits (variable.py:169-205, 262-275): a two-value tuple
+    excludes both limits; in a list, a limit wrapped in a tuple is
+    exclusive."""
     if vset is None:
-      vset = (-np.inf, np.inf)
-    vset = list(vset)
+      vset = [(-np.inf,), (np.inf,)]         # DEFAULT_VSETS[float]
+    if isinstance(vset, tuple):
+      if len(vset) != 2:
+        raise ValueError('Tuple vsets contain pairs of values, not '
+                         '{}'.format(vset))
+      vset = [(v,) for v in sorted(vset)]
     if len(vset) != 2:
       raise ValueError('float RV vset needs two limits, got {}'.format(vset))
     lims, incl = [], []
@@ -42,7 +74,9 @@ class RV:
       else:
         lims.append(float(v))
         incl.append(True)
-    self.vlims = np.array([min(lims), max(lims)])
+    if lims[1] < lims[0]:                    # variable.py:268-271 re-orders
+      lims, incl = lims[::-1], incl[::-1]
+    self.vlims = np.array(lims)
     self.lo_incl, self.hi_incl = incl[0], incl[1]
 
   def set_ufun(self, ufun=None, *args, **kwds):
@@ -52,6 +86,9 @@ class RV:
     if ufun is None:
       self._log_ufun = False
       return
+    if self.vtype is int:
+      raise NotImplementedError('RV {}: non-floats do not support '
+                                'transformation'.format(self.name))
     fwd, inv = ufun
     if fwd is not np.log or inv is not np.exp:
       raise NotImplementedError(
@@ -69,7 +106,10 @@ class RV:
 
   @property
   def length(self):
-    """max(ulims) - min(ulims) (variable.py:336)."""
+    """max(ulims) - min(ulims) (variable.py:336); the number of values for
+    an int variable (variable.py:327)."""
+    if self.vtype is int:
+      return float(self._int_len)
     ul = self.ulims
     return max(ul) - min(ul)
 

@@ -214,6 +214,9 @@ class SP:
     if self._update not in (None,) + ok or self._thresh not in (None,) + ok:
       raise L.NotLowerable('mixed scores/thresh/update samplers')
     prior = None
+    if joint and any(rv.vtype is int for rv in rvs):
+      raise L.NotLowerable('joint=True priors of int variables (a uniform '
+                           'over the value set) have no kernel')
     if joint:
       lens = [rv.length for rv in rvs]
       nl = [-np.log(L_) if np.isfinite(L_) else -np.inf for L_ in lens]
@@ -298,30 +301,151 @@ class SP:
             'vsets': vsets}
 
   def _lower_delta(self, rvs, names):
+    """Field.set_delta / eval_delta / apply_delta (field.py:220-317,
+    469-552; variable.py:600-739) lowered to a proposal spec."""
     delta, dargs, dkw = self._delta_spec()
+    if delta is None:
+      raise L.NotLowerable('set_delta() first')
+    if callable(delta) and not isinstance(delta, tuple):
+      if dkw:   # the reference hands these keywords to the callable itself
+        raise L.NotLowerable('keywords of a callable delta ({}) are the '
+                             "callable's own".format(sorted(dkw)))
+      return L.trace_delta(delta, names)
     scale = bool(dkw.get('scale', False))
-    if dkw.get('bound', False):
-      raise L.NotLowerable('bound=True deltas have no kernel')
-    if dargs:
-      raise L.NotLowerable('per-variable unscaled deltas have no kernel')
+    bound = bool(dkw.get('bound', False))
     lengths = np.array([rv.length for rv in rvs], np.float64)
-    if isinstance(delta, tuple):
-      if scale and not np.all(np.isfinite(lengths)):
-        raise ValueError('Cannot spherise variables with infinite length')
+    is_int = np.array([rv.vtype is int for rv in rvs])
+    d = len(rvs)
+    on = np.ones(d, np.int32)
+    if isinstance(delta, dict):
+      # field.py:261-263 converts the dict to a Delta but tests the ORIGINAL
+      # argument against the Delta type, so a dict takes the tuple branch
+      # (:308-316): no variable delta is set, eval_delta yields Delta(None,
+      # ...) and apply_delta returns the values unchanged, unbounded
+      unknown = set(delta) - set(names)
+      if unknown or len(delta) != d:
+        raise TypeError('Delta() fields {} do not match {}'.format(
+            sorted(delta), names))
+      unscale = dargs[0] if dargs else {}
+      for rv, L_ in zip(rvs, lengths):
+        if rv.name not in unscale and not np.isfinite(L_):
+          raise AssertionError('Cannot spherise Variable {} with infinite '
+                               'length'.format(rv.name))
+      return {'kind': 'vardelta', 'mode': np.zeros(d, np.int32),
+              'delta': np.zeros(d)}
+    if isinstance(delta, tuple) and hasattr(delta, '_fields'):
+      # a Delta instance: each variable's own delta (field.py:264-274)
+      if list(delta._fields) != list(names):
+        raise L.NotLowerable('Delta fields {} are not the process variables '
+                             '{}'.format(list(delta._fields), names))
+      if dargs:
+        raise AssertionError('Optional args prohibited for dict/delta '
+                             'instance inputs')
+      mode, steps = np.zeros(d, np.int32), np.zeros(d)
+      for i, el in enumerate(delta):
+        m, v = self._var_delta(el, rvs[i])
+        if m is None:          # delta None: apply_delta returns the value
+          on[i] = 0
+          continue
+        if m == 0 and scale:   # variable.py:637-639: only a bare scalar
+          if not np.isfinite(lengths[i]):
+            raise AssertionError('Cannot scale by infinite length')
+          v = v * lengths[i]
+        mode[i], steps[i] = m, v
+      prop = {'kind': 'vardelta', 'mode': mode, 'delta': steps}
+    elif isinstance(delta, tuple):
+      # spherical (field.py:308-316, 502-531)
+      unscale = dargs[0] if dargs else {}
+      if unscale:
+        # eval_delta then builds a Delta without the unscaled keys (or from
+        # the args tuple itself) and fails
+        raise TypeError('a spherical delta with unscaled variables {} is '
+                        'not constructible'.format(sorted(unscale)))
+      if len(delta) != 1:
+        raise AssertionError('Tuple delta must contain one element')
+      if not np.all(np.isfinite(lengths)):
+        bad = [rv.name for rv, L_ in zip(rvs, lengths) if not np.isfinite(L_)]
+        raise AssertionError('Cannot spherise Variable {} with infinite '
+                             'length'.format(bad[0]))
       d0 = float(delta[0])
       if scale:
         d0 = d0 * np.sqrt(np.sum(lengths ** 2))        # field.py:513-515
         mult = lengths
       else:
-        mult = np.ones(len(rvs))
-      return {'kind': 'sphere', 'delta': d0, 'lengths': mult}
-    if isinstance(delta, list):
-      d0 = float(delta[0])
-      dv = d0 * lengths if scale else np.full(len(rvs), d0)
-      return {'kind': 'uniform', 'delta': dv}
-    if callable(delta):
-      return L.trace_delta(delta, names)
-    raise L.NotLowerable('delta {} has no kernel'.format(delta))
+        mult = np.ones(d)
+      prop = {'kind': 'sphere', 'delta': d0, 'lengths': mult}
+    else:
+      # a bare scalar or a one-element list, per-variable overrides in
+      # args[0] exempt from scaling (field.py:276-306)
+      urand = isinstance(delta, list)
+      if urand:
+        if len(delta) != 1:
+          raise AssertionError('List delta requires a single element')
+        delta = delta[0]
+      if len(dargs) > 1 or (dargs and not isinstance(dargs[0], dict)):
+        raise AssertionError('Optional positional arguments must comprises a '
+                             'single dict')
+      unscale = dargs[0] if dargs else {}
+      extra_keys = set(unscale) - set(names)
+      if extra_keys:
+        raise TypeError('unexpected Delta fields {}'.format(sorted(extra_keys)))
+      mode, steps = np.zeros(d, np.int32), np.zeros(d)
+      for i, rv in enumerate(rvs):
+        val = unscale.get(rv.name, delta)
+        if scale and rv.name not in unscale:
+          if not np.isfinite(lengths[i]):
+            raise AssertionError('Cannot scale by infinite length for '
+                                 'Variable {}'.format(rv.name))
+          val = val * lengths[i]
+        m, v = self._var_delta([val] if urand else val, rvs[i])
+        if m is None:
+          on[i] = 0
+          continue
+        mode[i], steps[i] = m, v
+      if urand and not is_int.any() and np.all(mode == 2):
+        prop = {'kind': 'uniform', 'delta': steps}
+      else:
+        prop = {'kind': 'vardelta', 'mode': mode, 'delta': steps}
+    if is_int.any():
+      prop['vint'] = is_int.astype(np.int32)
+    if bound:
+      # variable.py:707-713: int limits always clamp; float tuple limits
+      # are exclusive
+      prop['bound'] = {
+          'on': on, 'lo': np.array([rv.vlims[0] for rv in rvs], np.float64),
+          'hi': np.array([rv.vlims[1] for rv in rvs], np.float64),
+          'xlo': np.array([0 if rv.vtype is int else int(not rv.lo_incl)
+                           for rv in rvs], np.int32),
+          'xhi': np.array([0 if rv.vtype is int else int(not rv.hi_incl)
+                           for rv in rvs], np.int32)}
+    return prop
+
+  @staticmethod
+  def _var_delta(el, rv):
+    """One variable's delta (variable.py:613-640) -> (mode, step): tuple ->
+    polarity, list -> uniform (randint for an int variable), bare scalar ->
+    fixed; None -> (None, 0)."""
+    if el is None:
+      return None, 0.
+    if callable(el):
+      raise L.NotLowerable('callable per-variable deltas have no kernel')
+    if isinstance(el, (tuple, list)):
+      if len(el) != 1:
+        raise AssertionError('{} delta must contain one element'.format(
+            'Tuple' if isinstance(el, tuple) else 'List'))
+      v = el[0]
+      if not np.isscalar(v):
+        raise AssertionError('Unrecognised delta type: {}'.format(v))
+      if isinstance(el, tuple):
+        return 1, float(v)
+      if rv.vtype is int:
+        if not int(v) >= 1:    # randint(-v, v) needs trunc(v) >= 1
+          raise ValueError('randint(-{0}, {0}): low >= high'.format(v))
+        return 3, float(v)
+      return 2, float(v)
+    if not np.isscalar(el):
+      raise AssertionError('Unrecognised delta type: {}'.format(el))
+    return 0, float(el)
 
   def _lower_tran(self, tran, names, scores, via_rf=False):
     if scores == 'metropolis':
@@ -485,16 +609,44 @@ class Sampler:
       out[:, i] = np.broadcast_to(np.asarray(init[k], np.float64), (n,))
     return out
 
+  def _cycle_rf(self):
+    """The RF whose conditional cycle this Gibbs run advances: the
+    reference keeps RF.__cond_mod per RF, so consecutive samplers on the same
+    RF continue mid-cycle (rf.py:446-452)."""
+    if self.spec.get('kind') == 'linreg':
+      tf = self.sp._tfun
+      return self.sp._subfield(tf) or tf
+    return self.sp._tran if isinstance(self.sp._tran, RF) else self.sp.roots
+
+  def _cycle_len(self):
+    if self.spec.get('kind') == 'linreg':
+      return 3
+    p = self.spec['proposal']
+    return -(-int(self.spec['dim']) // int(p['tsteps']))
+
   def run(self):
     if self.tr is not None:
       return self
     self.spec = self.sp.lower(self.extra, self.iid, self.joint)
     self.pscale = self.spec['pscale']
+    gibbs = self.spec.get('kind') == 'linreg' or \
+        self.spec['proposal']['kind'] == 'gibbs'
+    rf = self._cycle_rf() if gibbs else None
+    self.step0 = getattr(rf, '_pbh_cond_step', 0) if gibbs else 0
     if self.spec.get('kind') == 'linreg':
-      return self._run_linreg()
+      self._run_linreg()
+    else:
+      self._run_engine()
+    if gibbs:   # the RF's __cond_mod advances by one block per SP step
+      rf._pbh_cond_step = (self.step0 + self.stop) % self._cycle_len()
+    return self
+
+  def _run_engine(self):
     eng = Engine(self.spec, device=self.device)
     try:
       eng.init_chains(self._init_array())
+      if self.step0:
+        eng.set_step(self.step0)
       if self.rng == 'legacy':
         seeds = None if self.seeds is None else np.asarray(self.seeds)
         if seeds is None and self.batched:
@@ -503,7 +655,8 @@ class Sampler:
         if seeds is None:
           # one chain on NumPy's GLOBAL stream: drawn on the host so that the
           # global state advances exactly as the reference leaves it
-          streams = replay.legacy_streams(self.spec, self.stop, seeds)
+          streams = replay.legacy_streams(self.spec, self.stop, seeds,
+                                          step0=self.step0)
           eng.upload_replay(streams)
           th = streams[:, -1, :] if self.spec['proposal']['kind'] != 'gibbs' \
               else None
@@ -523,7 +676,6 @@ class Sampler:
       self.moments = eng.moments()
     finally:
       eng.close()
-    return self
 
   def _run_linreg(self):
     from probayes_amd import linreg
@@ -536,17 +688,18 @@ class Sampler:
       if self.batched and self.seeds is None:
         raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
       rand = linreg.legacy_streams(self.stop, n_obs, sp['hyper'][4],
-                                   None if self.seeds is None else self.seeds)
+                                   None if self.seeds is None else self.seeds,
+                                   step0=self.step0)
       rng = 'replay'
     out = linreg.run(sp['x_obs'], sp['y_obs'], self._init_array(), self.stop,
                      hyper=sp['hyper'], vsets=sp['vsets'], rng=rng,
-                     seed=self.seed, rand=rand, device=self.device)
+                     seed=self.seed, rand=rand, device=self.device,
+                     step0=self.step0)
     vx, vp = out['v_x'], out['v_p']
     # gibbs: p = v, u = True, s = t = None (sp_utils.py:75-84)
     self.tr = {'v_x': vx, 'v_p': vp, 'p_x': vx, 'p_p': vp,
                'u': np.ones(vp.shape, np.uint8)}
     self.moments = None
-    return self
 
   def __iter__(self):
     self.run()

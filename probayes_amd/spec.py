@@ -16,6 +16,11 @@ encodes the closed set of model forms the engine lowers:
   proposal kind gauss   callable Delta(norm.rvs(loc, scale)) per dim
                 sphere  tuple delta (field.py:509-531)
                 uniform list delta (variable.py:625-633)
+                vardelta per-variable modes (fixed 0 | polarity 1 | uniform 2 |
+                        randint 3) and steps: a Delta of containers or a bare
+                        scalar Field delta (field.py:266-306, variable.py:600-640)
+                (any MH kind may carry vint [d]: int variables, truncated,
+                 and bound {on, lo, hi, xlo, xhi}: bound=True, variable.py:700-739)
                 (any of the three may carry tfun [d, d]: the covariance
                 random walk delta' = tfun . delta, rf.py:210-220, 340-354)
                 gibbs   CondCov conditional sampling (cond_cov.py:22-65)
@@ -25,7 +30,7 @@ encodes the closed set of model forms the engine lowers:
 import numpy as np
 
 TARGETS = ('diag_gauss', 'norm_iid', 'gmm', 'norm_pdf', 'uniform_pdf', 'mvn')
-PROPOSALS = ('gauss', 'sphere', 'uniform', 'gibbs')
+PROPOSALS = ('gauss', 'sphere', 'uniform', 'gibbs', 'vardelta')
 SCORES = ('hastings', 'metropolis', 'gibbs')
 
 
@@ -99,6 +104,11 @@ def make_spec(dim, target, proposal, scores='hastings', pscale=None,
     proposal['lengths'] = _vec(proposal.get('lengths', 1.), d, 'lengths')
   elif pk == 'uniform':
     proposal['delta'] = _vec(proposal['delta'], d, 'delta')
+  elif pk == 'vardelta':
+    proposal['delta'] = _vec(proposal['delta'], d, 'delta')
+    proposal['mode'] = np.asarray(proposal['mode'], np.int32).reshape(d)
+    if np.any((proposal['mode'] < 0) | (proposal['mode'] > 3)):
+      raise ValueError('vardelta modes are 0..3')
   elif pk == 'gibbs':
     proposal['mean'] = _vec(proposal['mean'], d, 'mean')
     proposal['cov'] = np.asarray(proposal['cov'], np.float64).reshape(d, d)
@@ -112,6 +122,16 @@ def make_spec(dim, target, proposal, scores='hastings', pscale=None,
     if tf.shape != (d, d) or not np.all(np.isfinite(tf)):
       raise ValueError('tfun must be a finite [{0}, {0}] matrix'.format(d))
     proposal['tfun'] = tf
+  if pk != 'gibbs':
+    if proposal.get('vint') is not None:
+      proposal['vint'] = np.asarray(proposal['vint'], np.int32).reshape(d)
+    if proposal.get('bound') is not None:
+      b = dict(proposal['bound'])
+      b['lo'], b['hi'] = _vec(b['lo'], d, 'bound.lo'), _vec(b['hi'], d, 'bound.hi')
+      for key in ('on', 'xlo', 'xhi'):
+        b[key] = np.asarray(b.get(key, [1 if key == 'on' else 0] * d),
+                            np.int32).reshape(d)
+      proposal['bound'] = b
   if tran is None:
     tran = {'kind': 'const', 'value': 1.0, 'sym': True}
   tran = dict(tran)

@@ -384,3 +384,118 @@ def gibbs_linreg(pb, params):
 # user-tfun Gibbs: lowered by probayes_amd.linreg, not the generic spec
 # (oracle/linreg.py, tests/test_linreg.py)
 TFUN_WORKLOADS = {'gibbs_linreg': (gibbs_linreg, _linreg_params(), 8, 96, 14000)}
+
+
+# ----------------------------------------------------------------------------
+# Delta forms beyond the callable / plain tuple / plain list:
+# bound=True (variable.py:700-739: clamp closed limits, bounce exclusive
+# ones), per-variable dict deltas (field.py:266-274, variable.py:600-640:
+# tuple = random polarity, list = uniform or, for int variables, randint,
+# bare scalar = fixed step), the unscaled-override dict args[0]
+# (field.py:276-306) and bare scalar Field deltas.  The models restate
+# examples/omc/omc_rw_circle.py:16-22 (tuple vsets, spherical delta,
+# bound=True) and examples/markov/markov_delta.py:32 (list delta, scale and
+# bound) on small diagonal-Gaussian densities so that chains reach the limits.
+# ----------------------------------------------------------------------------
+def _diag_lp(keys, mus, sigmas):
+  def lp(**kw):
+    return sum(scipy.stats.norm.logpdf(kw[k], mus[i], sigmas[i])
+               for i, k in enumerate(keys))
+  return lp
+
+
+def _delta_model(pb, rvs, mus, sigmas, init):
+  keys = [v.name for v in rvs]
+  process = pb.SP(pb.RF(*rvs))
+  process.set_prob(_diag_lp(keys, mus, sigmas), pscale='log')
+  process.set_tran(lambda **kw: 1.)
+  process.set_scores('hastings')
+  process.set_update('metropolis')
+  return process, dict(zip(keys, init)), None, {}, keys
+
+
+def bound_sphere2(pb, params):
+  """omc_rw_circle.py:16-22: tuple vsets (both limits exclusive) and
+  set_delta((0.15 r,), bound=True) -> proposals leaving the box bounce back."""
+  x = pb.RV('x', vtype=float, vset=(-1., 1.))
+  y = pb.RV('y', vtype=float, vset=(-1., 1.))
+  out = _delta_model(pb, [x, y], [0.7, -0.6], [0.4, 0.5], [0., 0.])
+  out[0].set_delta((params['step'],), bound=True)
+  return out
+
+
+def _three_vsets(pb):
+  return [pb.RV('x', vtype=float, vset=[(-1.,), 1.]),    # lower exclusive
+          pb.RV('y', vtype=float, vset=[-1., (1.,)]),    # upper exclusive
+          pb.RV('z', vtype=float, vset=[0., 2.])]        # closed
+
+
+def bound_list3(pb, params):
+  """markov_delta.py:32 form on a field: set_delta([d], {'z': [dz]},
+  scale=True, bound=True): uniform deltas scaled by length except the
+  unscaled override, one-sided bounces and a clamp."""
+  out = _delta_model(pb, _three_vsets(pb), [-0.8, 0.8, 1.9], [0.5, 0.5, 0.6],
+                     [0., 0., 1.])
+  out[0].set_delta([0.2], {'z': 0.15}, scale=True, bound=True)
+  return out
+
+
+def pervar3(pb, params):
+  """Per-variable deltas as a Delta instance (field.py:266-274): x random
+  polarity, y uniform, z a fixed step scaled by its length, all bounded."""
+  out = _delta_model(pb, _three_vsets(pb), [-0.8, 0.8, 1.9], [0.5, 0.5, 0.6],
+                     [0., 0., 1.])
+  p = out[0]
+  p.set_delta(p.Delta(x=(0.25,), y=[0.3], z=0.05), scale=True, bound=True)
+  return out
+
+
+def dict3(pb, params):
+  """A dict delta: field.py:262-263 converts it to a Delta but tests the
+  ORIGINAL argument, so it takes the tuple (spherise) branch with no
+  per-variable deltas set; eval_delta then yields Delta(None, ...) and
+  apply_delta leaves every value unchanged (variable.py:660-672)."""
+  out = _delta_model(pb, _three_vsets(pb), [-0.8, 0.8, 1.9], [0.5, 0.5, 0.6],
+                     [0.1, 0.2, 1.])
+  out[0].set_delta({'x': (0.25,), 'y': [0.3], 'z': 0.05}, bound=True)
+  return out
+
+
+def fixed2(pb, params):
+  """Bare scalar Field delta (fixed step) with an unscaled override."""
+  x = pb.RV('x', vtype=float, vset=[-1., 1.])
+  y = pb.RV('y', vtype=float, vset=[-1., 1.])
+  out = _delta_model(pb, [x, y], [0.3, -0.2], [0.5, 0.4], [0., 0.])
+  out[0].set_delta(0.02, {'y': -0.03}, scale=True, bound=True)
+  return out
+
+
+def randint2(pb, params):
+  """An int variable's list delta draws np.random.randint(-d, d)
+  (variable.py:630-631); a zero draw is redrawn once by apply_delta's
+  `delta or self._delta` (variable.py:660-667); bound clamps the int to its
+  value-set limits."""
+  n = pb.RV('n', vtype=int, vset=range(0, 21))
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  out = _delta_model(pb, [n, x], [12., 0.], [3., 1.], [0, 0.])
+  p = out[0]
+  p.set_delta(p.Delta(n=[3], x=[0.5]), bound=True)
+  return out
+
+
+DELTA_WORKLOADS = {
+  'bound_sphere2': (bound_sphere2, {'step': 0.15}, 16, 256, 15000),
+  'bound_list3': (bound_list3, {}, 16, 256, 16000),
+  'pervar3': (pervar3, {}, 16, 256, 17000),
+  'fixed2': (fixed2, {}, 8, 128, 18000),
+  'dict3': (dict3, {}, 8, 64, 18500),
+  'randint2': (randint2, {}, 16, 256, 19000),
+}
+
+# Consecutive samplers on ONE process share the RF's CondCov cycle phase
+# (rf.py:446-452 __cond_mod) and NumPy's global stream: name -> (base
+# workload, segment lengths, chains)
+SEGMENTED = {
+  'gibbs_norm2d_seg': ('gibbs_norm2d', (7, 10), 6),
+  'gibbs_linreg_seg': ('gibbs_linreg', (4, 5, 7), 4),
+}

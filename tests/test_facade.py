@@ -11,7 +11,9 @@ import pytest
 
 import oracle
 import probayes_amd as pb
-from mcmc_examples import WORKLOADS
+from mcmc_examples import WORKLOADS as _W, DELTA_WORKLOADS
+
+WORKLOADS = dict(_W, **DELTA_WORKLOADS)
 
 
 def _spec_equal(a, b, path=''):
@@ -90,19 +92,15 @@ def test_example_scripts_reproduce_reference_chains(name):
     assert summary.u.count(True) == int(g['u'][c].sum())
     # the global legacy stream advanced exactly as the reference's did
     spec = oracle.golden_spec(name, g)
-    ref_stream = oracle.legacy_streams(spec, g['seeds'][c:c + 1], t + 1)
-    nxt = ref_stream[t, 0, 0]
-    if spec['proposal']['kind'] == 'gauss':   # next draw would be a gauss
-      rs = np.random.RandomState(int(g['seeds'][c]))
-      for _ in range(t):
-        rs.standard_normal(len(keys)); rs.random_sample()
-      nxt = rs.random_sample()
-    assert np.random.random_sample() == nxt
+    states = []
+    oracle.legacy_streams(spec, g['seeds'][c:c + 1], t, states=states)
+    assert np.random.random_sample() == states[0].random_sample()
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('name', ['metrohast_norm1d', 'diag10', 'gibbs8',
-                                  'gmm2', 'mcmc_prob6'])
+                                  'gmm2', 'mcmc_prob6', 'bound_sphere2',
+                                  'bound_list3', 'pervar3', 'randint2'])
 def test_batched_sampler_reproduces_all_reference_chains(name):
   builder, params, n, t, seed0 = WORKLOADS[name]
   process, init, extra, kwds, keys, g = _build(name)
@@ -176,3 +174,78 @@ def test_summary_conditionalise_fails_as_reference():
   assert process(samples).v is not None
   with pytest.raises(TypeError):
     process(samples, conditionalise=True)
+
+
+def test_delta_forms_lower_and_fail_like_the_reference():
+  """field.py:220-317 / variable.py:376-410 argument handling: the
+  reference's assertion and construction errors, and NotLowerable for the
+  forms without a kernel."""
+  x = pb.RV('x', vtype=float, vset=[-1., 1.])
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  n = pb.RV('n', vtype=int, vset=range(5))
+  assert (x.lo_incl, x.hi_incl, y.lo_incl, y.hi_incl) == (True, True, False, False)
+  assert n.length == 5 and list(n.vlims) == [0., 4.]
+  r = pb.RV('r', vtype=float, vset=[(3.,), 1.])    # re-ordered limits
+  assert list(r.vlims) == [1., 3.] and r.lo_incl and not r.hi_incl
+
+  def proc(*rvs):
+    p = pb.SP(pb.RF(*rvs))
+    keys = [v.name for v in rvs]
+    p.set_prob(lambda **kw: sum(__import__('scipy').stats.norm.logpdf(kw[k])
+                                for k in keys), pscale='log')
+    p.set_tran(lambda **kw: 1.)
+    p.set_scores('hastings')
+    return p
+
+  p = proc(x, y)
+  p.set_delta((0.1,), scale=True)
+  with pytest.raises(AssertionError):     # y has infinite length
+    p.lower()
+  p.set_delta([0.1], scale=True)
+  with pytest.raises(AssertionError):
+    p.lower()
+  p.set_delta([0.1], {'y': 0.3}, scale=True, bound=True)
+  prop = p.lower()['proposal']
+  assert prop['kind'] == 'uniform' and list(prop['delta']) == [0.2, 0.3]
+  assert list(prop['bound']['xlo']) == [0, 1]
+  p.set_delta((0.1,), {'y': 0.3})
+  with pytest.raises(TypeError):
+    p.lower()
+  p.set_delta(p.Delta(x=(0.1,), y=None), bound=True)
+  prop = p.lower()['proposal']
+  assert list(prop['mode']) == [1, 0] and list(prop['bound']['on']) == [1, 0]
+  p.set_delta(p.Delta(x=lambda: 0.1, y=[0.2]))
+  with pytest.raises(pb.NotLowerable):
+    p.lower()
+  q = proc(n, x)
+  q.set_delta(q.Delta(n=[0.5], x=[0.1]))
+  with pytest.raises(ValueError):         # randint(0, 0)
+    q.lower()
+  q.set_delta([2], scale=False)
+  prop = q.lower()['proposal']
+  assert prop['kind'] == 'vardelta' and list(prop['mode']) == [3, 2]
+  assert list(prop['vint']) == [1, 0]
+  with pytest.raises(pb.NotLowerable):    # uniform prior over an int vset
+    q.lower(joint=True)
+  q.set_delta(lambda: q.Delta(n=1, x=0.), bound=True)
+  with pytest.raises(pb.NotLowerable):
+    q.lower()
+
+
+@pytest.mark.gpu
+def test_consecutive_samplers_continue_the_cycle():
+  """Two samplers on one process, as tools/gen_golden.py ran the reference
+  (gibbs_norm2d_seg): the second starts at the RF's CondCov phase
+  (rf.py:446-452) on NumPy's continuing global stream."""
+  from mcmc_examples import SEGMENTED
+  base, segs, n = SEGMENTED['gibbs_norm2d_seg']
+  g = oracle.load_golden('gibbs_norm2d_seg')
+  builder, params = _W[base][:2]
+  for c in range(n):
+    process, init, extra, kwds, keys = builder(pb, params)
+    np.random.seed(int(g['seeds'][c]))
+    got = []
+    for stop in segs:
+      summary = process(process.walk(process.sampler(init, stop=stop, **kwds)))
+      got.append(np.stack([np.asarray(summary.v[k]) for k in keys], -1))
+    assert _golden_rtol(np.concatenate(got), g['v_x'][c]) <= 1e-12

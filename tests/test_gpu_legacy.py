@@ -47,6 +47,18 @@ def _specs():
   su = oracle.golden_spec('diag10')
   su['proposal'] = {'kind': 'uniform', 'delta': np.full(10, 0.3)}
   out['uniform10'] = su
+  # per-variable deltas: randint (NumPy's masked rejection on 32-bit words,
+  # small and wide ranges, a float bound truncated), polarity, fixed
+  for name in ('randint2', 'pervar3'):
+    out[name] = oracle.golden_spec(name)
+  sv = oracle.golden_spec('diag10')
+  sv.update(dim=4, names=['a', 'b', 'c', 'e'])
+  sv['target'] = {'kind': 'diag_gauss', 'mu': np.zeros(4), 'sigma': np.ones(4)}
+  sv['proposal'] = {'kind': 'vardelta', 'mode': np.array([3, 3, 1, 0], np.int32),
+                    'delta': np.array([1000., 70000.5, 0.3, 0.2]),
+                    'vint': np.array([1, 1, 0, 0], np.int32)}
+  sv['ufun'] = np.zeros(4, np.int32)
+  out['randint_wide'] = sv
   return out
 
 

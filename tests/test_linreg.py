@@ -247,3 +247,43 @@ def test_lane_pair_kernel_equals_one_lane_kernel(monkeypatch):
     assert np.array_equal(a['v_p'], b['v_p'])
     assert np.array_equal(a['final_x'], b['final_x'])
     assert np.array_equal(a['final_p'], b['final_p'])
+
+
+@pytest.mark.gpu
+def test_consecutive_samplers_continue_the_cycle(root):
+  """Three samplers on one process (gibbs_linreg_seg, recorded from the
+  reference): each continues the paras RF's __cond_mod (rf.py:446-452) and
+  NumPy's global stream."""
+  import os
+  import probayes_amd as pb
+  from mcmc_examples import TFUN_WORKLOADS
+  g = np.load(os.path.join(root, 'tests/golden/gibbs_linreg_seg.npz'))
+  builder, params = TFUN_WORKLOADS['gibbs_linreg'][:2]
+  params = dict(params, cond=linreg.LinRegConditional)
+  for c in range(len(g['seeds'])):
+    process, init, extra, kwds, keys = builder(pb, params)
+    np.random.seed(int(g['seeds'][c]))
+    got = []
+    for stop in g['segments']:
+      s = process(process.walk(process.sampler(init, extra, stop=int(stop),
+                                               **kwds)))
+      got.append(np.stack([np.asarray(s.v[k]) for k in keys], -1))
+    got = np.concatenate(got)
+    assert np.max(np.abs(got - g['v_x'][c]) /
+                  np.maximum(np.abs(g['v_x'][c]), 1.)) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_fast_form_is_stable_at_large_offsets():
+  """The PHILOX form's centred sufficient statistics (x, y offset by 1e3):
+  same chains as the reference arithmetic of PHILOX_F64 on the same draws."""
+  rs = np.random.RandomState(2)
+  x = 1000. + rs.normal(0, 1, 60)
+  y = 2. + 0.004 * x + rs.normal(0, 0.5, 60)
+  n, t = 2048, 120
+  init = np.tile([2.0, 0.004, 0.5], (n, 1))
+  a = linreg.run(x, y, init, t, rng='philox', seed=4, vsets=None)
+  b = linreg.run(x, y, init, t, rng='philox_f64', seed=4, vsets=None)
+  rel = np.abs(a['v_x'] - b['v_x']) / np.maximum(np.abs(b['v_x']), 1.)
+  assert rel.max() <= 1e-9, rel.max()
+  assert np.max(np.abs(a['v_p'] - b['v_p']) / np.abs(b['v_p'])) <= 1e-9

@@ -48,8 +48,10 @@ def _pb():
   return pb
 
 
-from mcmc_examples import WORKLOADS, TFUN_WORKLOADS  # noqa: E402
-WORKLOADS = dict(WORKLOADS, **TFUN_WORKLOADS)  # builders shared with tests
+from mcmc_examples import WORKLOADS, TFUN_WORKLOADS, DELTA_WORKLOADS, \
+    SEGMENTED  # noqa: E402
+# builders shared with tests
+WORKLOADS = dict(WORKLOADS, **TFUN_WORKLOADS, **DELTA_WORKLOADS)
 
 
 def _nan(v):
@@ -57,16 +59,26 @@ def _nan(v):
 
 
 def run(name):
+  """One workload; a SEGMENTED name runs its base workload's consecutive
+  samplers (same process, same init, NumPy's global stream continuing)."""
   pb = _pb()
-  builder, params, n_chains, n_steps, seed0 = WORKLOADS[name]
+  segments = None
+  if name in SEGMENTED:
+    base, segments, n_chains = SEGMENTED[name]
+    builder, params, _, _, seed0 = WORKLOADS[base]
+    n_steps = int(sum(segments))
+  else:
+    builder, params, n_chains, n_steps, seed0 = WORKLOADS[name]
   keys = None
   arrs = {k: [] for k in ['v_x', 'v_p', 'p_x', 'p_p', 's', 't', 'u']}
   for c in range(n_chains):
     process, init, extra, kwds, keys = builder(pb, params)
     np.random.seed(seed0 + c)
     args = (init,) if extra is None else (init, extra)
-    sampler = process.sampler(*args, stop=n_steps, **kwds)
-    samples = list(process.walk(sampler))
+    samples = []
+    for stop in (segments or (n_steps,)):
+      sampler = process.sampler(*args, stop=stop, **kwds)
+      samples += list(process.walk(sampler))
     assert len(samples) == n_steps
     arrs['v_x'].append([[float(s.v[k]) for k in keys] for s in samples])
     arrs['v_p'].append([float(s.v.prob) for s in samples])
@@ -76,12 +88,15 @@ def run(name):
     arrs['t'].append([_nan(s.t) for s in samples])
     arrs['u'].append([1 if s.u else 0 for s in samples])
     # The summary path (sp.py:131-198) must agree with the per-step fields.
-    summary = process(samples)
-    assert np.array_equal(np.ravel(summary.v[keys[0]]),
+    summary = process(samples if segments is None else samples[-segments[-1]:])
+    if segments is None:
+      assert np.array_equal(np.ravel(summary.v[keys[0]]),
                           np.array(arrs['v_x'][-1])[:, 0])
-    assert summary.u.count(True) == sum(arrs['u'][-1])
+      assert summary.u.count(True) == sum(arrs['u'][-1])
   out = {k: np.array(v, dtype=np.uint8 if k == 'u' else np.float64)
          for k, v in arrs.items()}
+  if segments is not None:
+    out['segments'] = np.array(segments, np.int64)
   out['seeds'] = np.arange(seed0, seed0 + n_chains, dtype=np.int64)
   out['keys'] = np.array(keys)
   for k, v in params.items():
@@ -97,7 +112,7 @@ def run(name):
 
 
 if __name__ == '__main__':
-  names = sys.argv[1:] or list(WORKLOADS)
+  names = sys.argv[1:] or list(WORKLOADS) + list(SEGMENTED)
   for n in names:
     import time
     t0 = time.time()
