@@ -11,8 +11,9 @@ norm.logpdf(y, b0 + b1 x, y_sigma) plus the joint uniform root priors
 `LinRegConditional` is a plain callable with cond_reg's signature and
 NumPy-global draws, so the SAME object runs in the reference as the user tfun;
 the façade (`SP.lower`) recognises it and lowers the process to
-`pbh_linreg_gibbs` (probayes_amd/csrc/pbh_linreg.hip).  Other user tfuns raise
-NotLowerable.  `run` is the batched entry: all chains in one kernel launch.
+`pbh_linreg_gibbs` (probayes_amd/csrc/pbh_linreg.hip).  A user's own cond_reg
+(the example's closure) is identified by probing (identify_conditional); other
+user tfuns raise NotLowerable.  `run` is the batched entry: all chains in one kernel launch.
 """
 import ctypes
 
@@ -127,6 +128,100 @@ def legacy_streams(n_steps, n_obs, y_sigma_alpha, seeds=None, step0=0):
       out[t, c] = g.standard_gamma(alpha) if (step0 + t) % 3 == 2 \
           else g.standard_normal()
   return out
+
+
+class _Recorder:
+  """Stands in for np.random.normal / np.random.gamma while a user
+  conditional is probed: records the arguments, returns a chosen value."""
+
+  def __init__(self, value):
+    self.value, self.calls = value, []
+
+  def __call__(self, *args, **kwds):
+    if kwds.get('size') is not None:
+      raise ValueError('size= in a conditional draw')
+    self.calls.append((args, kwds))
+    return self.value
+
+
+def _probe(fn, x_obs, y_obs, vals, unknown, z=0.6180339887498949,
+           g=1.7320508075688772):
+  """fn(x, y, **vals, unknown) with NumPy's normal / gamma recorded:
+  (draw kind, (loc, scale) or (shape, scale), output, the stub value)."""
+  normal, gamma = _Recorder(z), _Recorder(g)
+  saved = np.random.normal, np.random.gamma
+  np.random.normal, np.random.gamma = normal, gamma
+  try:
+    out = fn(x=x_obs, y=y_obs, unknown=unknown, **vals)
+  finally:
+    np.random.normal, np.random.gamma = saved
+  if len(normal.calls) + len(gamma.calls) != 1:
+    raise ValueError('expected exactly one draw')
+  kind, rec = ('normal', normal) if normal.calls else ('gamma', gamma)
+  args, kwds = rec.calls[0]
+  names = ('loc', 'scale') if kind == 'normal' else ('shape', 'scale')
+  full = dict(zip(names, args))
+  full.update(kwds)
+  return kind, (float(full[names[0]]), float(full.get('scale', 1.))), \
+      float(out), rec.value
+
+
+def _snap(v):
+  """A hyper-parameter recovered by probing, rounded to 12 significant
+  digits (the user wrote a short literal; verification decides)."""
+  return float('{:.12g}'.format(v))
+
+
+def identify_conditional(fn, x_obs, y_obs, n_probe=4):
+  """Hyper-parameters (b0_mu, b0_sigma, b1_mu, b1_sigma, alpha, beta) of a
+  user conditional with cond_reg's law (gibbs_linreg.py:34-62), found by
+  PROBING it: np.random.normal / gamma are replaced by recorders, the
+  callable is run at chosen parameter values, and the draw arguments it
+  passes identify the hyper-parameters (at y_sigma = inf the data terms
+  vanish: scale = beta_k_sigma, loc = beta_k_mu).  The identified form is
+  then verified at random points against LinRegConditional -- draw
+  arguments within 1e-12 relative and the output transform (the draw
+  itself, or 1 / sqrt(gamma draw)) exact.  Raises NotLowerable otherwise."""
+  from probayes_amd.lower import NotLowerable
+  x_obs = np.asarray(x_obs, np.float64)
+  y_obs = np.asarray(y_obs, np.float64)
+  n = len(x_obs)
+  try:
+    with np.errstate(divide='ignore', invalid='ignore', over='ignore'):
+      hyper = []
+      for key, other in (('beta_0', 'beta_1'), ('beta_1', 'beta_0')):
+        vals = {'beta_0': 0.3, 'beta_1': -0.2, 'y_sigma': np.inf}
+        kind, (loc, scale), _, _ = _probe(fn, x_obs, y_obs, vals, key)
+        if kind != 'normal':
+          raise ValueError('{} must be a normal draw'.format(key))
+        hyper += [_snap(loc), _snap(scale)]
+      vals = {'beta_0': 0.3, 'beta_1': -0.2, 'y_sigma': 1.}
+      kind, (shape, scale), _, _ = _probe(fn, x_obs, y_obs, vals, 'y_sigma')
+      if kind != 'gamma':
+        raise ValueError('y_sigma must be a gamma draw')
+      r = y_obs - 0.3 - -0.2 * x_obs
+      hyper += [_snap(shape - 0.5 * n), _snap(1 / scale - 0.5 * np.sum(r ** 2))]
+      ref = LinRegConditional(n, *hyper)
+      rs = np.random.RandomState(2024)
+      for _ in range(n_probe):
+        vals = {'beta_0': rs.uniform(-3, 3), 'beta_1': rs.uniform(-3, 3),
+                'y_sigma': rs.uniform(0.05, 4.)}
+        for key in KEYS:
+          got = _probe(fn, x_obs, y_obs, vals, key)
+          want = _probe(ref, x_obs, y_obs, vals, key)
+          if got[0] != want[0] or got[2] != want[2]:
+            raise ValueError('{}: different draw or output transform'.format(key))
+          a, b = np.array(got[1]), np.array(want[1])
+          if not np.all(np.abs(a - b) <= 1e-12 * np.abs(b)):
+            raise ValueError('{}: draw arguments {} != {}'.format(key, a, b))
+  except NotLowerable:
+    raise
+  except Exception as e:   # noqa: BLE001 -- any failure: not this form
+    raise NotLowerable('user tfun is not the linear-regression conditional '
+                       '(gibbs_linreg.py cond_reg): {}'.format(e))
+  if not (hyper[1] > 0 and hyper[3] > 0 and hyper[4] > 0):
+    raise NotLowerable('identified hyper-parameters {} are invalid'.format(hyper))
+  return tuple(hyper)
 
 
 def identify_loglik(prob, x_obs, y_obs, n_probe=3):

@@ -16,6 +16,10 @@ Recognised forms
          prod of norm.pdf(kw[k'], loc=kw[k] + off, scale=s)      -> gauss_pdf
   prob   sum_k norm.logpdf(kw[k], mu_k, sigma_k) (dims in order) -> diag_gauss
          prod_k uniform.pdf(kw[k], lo_k, scale_k)                -> uniform_pdf
+         a = logw + sum_i norm.logpdf(kw[k_i], mu[:, i], sd) (vectors over
+         components), then m = np.max(a); m + np.log(np.sum(np.exp(a - m)))
+         or scipy.special.logsumexp(a)                          -> gmm
+         (traced through NumPy's __array_ufunc__ / __array_function__)
   plus the scipy objects themselves (norm.pdf/logpdf, uniform.pdf,
   multivariate_normal) and the descriptor callables of probayes_amd.models.
 """
@@ -268,6 +272,135 @@ def trace_prob(fn, keys):
             'lo': np.array([_num(t.loc, 'loc') for t in terms]),
             'scale': np.array([_num(t.scale, 'scale') for t in terms])}, 'lin'
   raise NotLowerable('density is not a recognised form')
+
+
+# ---------------------------------------------------------------------------
+# prob: log-sum-exp mixtures, traced through NumPy's dispatch protocols
+# ---------------------------------------------------------------------------
+class Node:
+  """A symbolic array value: NumPy ufuncs and np.max / np.sum on it build a
+  graph instead of computing (NEP 13 / NEP 18 dispatch)."""
+  __array_priority__ = 1000
+
+  def __init__(self, op, *args):
+    self.op, self.args = op, args
+
+  _UFUNCS = {np.add: 'add', np.subtract: 'sub', np.exp: 'exp', np.log: 'log'}
+
+  def __array_ufunc__(self, ufunc, method, *inputs, **kw):
+    if method != '__call__' or kw or ufunc not in self._UFUNCS:
+      raise NotLowerable('{}.{} in a density'.format(ufunc.__name__, method))
+    return Node(self._UFUNCS[ufunc], *inputs)
+
+  def __array_function__(self, func, types, args, kwargs):
+    if kwargs or len(args) != 1:
+      raise NotLowerable('{} with options in a density'.format(func.__name__))
+    if func in (np.max, np.amax):
+      return Node('max', args[0])
+    if func is np.sum:
+      return Node('sum', args[0])
+    raise NotLowerable('{} in a density'.format(func.__name__))
+
+  def __add__(self, o):
+    return Node('add', self, o)
+
+  def __radd__(self, o):
+    return Node('add', o, self)
+
+  def __sub__(self, o):
+    return Node('sub', self, o)
+
+  def __rsub__(self, o):
+    return Node('sub', o, self)
+
+
+def _same(a, b):
+  """Structural equality of traced values."""
+  if a is b:
+    return True
+  if isinstance(a, Node) and isinstance(b, Node):
+    return a.op == b.op and len(a.args) == len(b.args) and \
+        all(_same(x, y) for x, y in zip(a.args, b.args))
+  if isinstance(a, Node) or isinstance(b, Node):
+    return False
+  return np.array_equal(np.asarray(a), np.asarray(b))
+
+
+def _lse_operand(out):
+  """A from m + log(sum(exp(A - m))) with m = max(A), or logsumexp(A)."""
+  if isinstance(out, Node) and out.op == 'lse':
+    return out.args[0]
+  if not (isinstance(out, Node) and out.op == 'add' and len(out.args) == 2):
+    return None
+  m, lg = out.args
+  if not (isinstance(m, Node) and m.op == 'max'):
+    return None
+  A = m.args[0]
+  ok = isinstance(lg, Node) and lg.op == 'log' and \
+      isinstance(lg.args[0], Node) and lg.args[0].op == 'sum'
+  ex = lg.args[0].args[0] if ok else None
+  ok = ok and isinstance(ex, Node) and ex.op == 'exp'
+  df = ex.args[0] if ok else None
+  ok = ok and isinstance(df, Node) and df.op == 'sub' and \
+      _same(df.args[0], A) and _same(df.args[1], m)
+  return A if ok else None
+
+
+def trace_logsumexp(fn, keys):
+  """A log-sum-exp Gaussian mixture written with NumPy (SURVEY App. B H5:
+  a = logw + logpdf(x, mu[:, 0], sd) + ...; m + log(sum(exp(a - m))))
+  -> gmm target with the SAME summation order, or NotLowerable."""
+  import scipy.special
+
+  def logpdf(*args, **kwds):
+    x = args[0] if args else kwds.pop('x')
+    loc, scale = _loc_scale(args[1:], kwds)
+    return Node('logpdf', x, loc, scale)
+
+  def lse(a, *args, **kwds):
+    if args or kwds:
+      raise NotLowerable('logsumexp with options in a density')
+    return Node('lse', a)
+
+  kw = {k: Node('var', k) for k in keys}
+  with _patched(scipy.stats.norm, logpdf=logpdf), \
+       _patched(scipy.special, logsumexp=lse):
+    try:
+      out = fn(**kw)
+    except NotLowerable:
+      raise
+    except Exception as e:
+      raise NotLowerable('density callable not traceable: {}'.format(e))
+  A = _lse_operand(out)
+  if A is None:
+    raise NotLowerable('density is not a log-sum-exp of component terms')
+  terms = []                       # left-associated a = c + t_0 + t_1 + ...
+  while isinstance(A, Node) and A.op == 'add':
+    terms.append(A.args[1])
+    A = A.args[0]
+  terms.append(A)
+  terms = terms[::-1]
+  d = len(keys)
+  if len(terms) != d + 1 or isinstance(terms[0], Node):
+    raise NotLowerable('mixture must be logw + one logpdf per variable')
+  logw = np.asarray(terms[0], np.float64).reshape(-1)
+  K = logw.size
+  mu = np.empty((K, d))
+  sd = None
+  for i, t in enumerate(terms[1:]):
+    if not (isinstance(t, Node) and t.op == 'logpdf' and
+            isinstance(t.args[0], Node) and t.args[0].op == 'var' and
+            t.args[0].args[0] == keys[i]):
+      raise NotLowerable('mixture terms must be logpdf(x_i, ...) in order')
+    _, loc, scale = t.args
+    if isinstance(loc, Node) or isinstance(scale, Node):
+      raise NotLowerable('mixture loc / scale must be constants')
+    mu[:, i] = np.broadcast_to(np.asarray(loc, np.float64), (K,))
+    s = np.broadcast_to(np.asarray(scale, np.float64), (K,))
+    if sd is not None and not np.array_equal(s, sd):
+      raise NotLowerable('mixture sds must be shared across variables')
+    sd = np.array(s)
+  return {'kind': 'gmm', 'logw': logw, 'mu': mu, 'sd': sd}, 'log'
 
 
 def is_same_callable(a, b):

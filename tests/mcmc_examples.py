@@ -192,8 +192,6 @@ def gmm2(pb, params):
                scipy.stats.norm.logpdf(kw['y'], mu[:, 1], sd)
     m = np.max(a)
     return m + np.log(np.sum(np.exp(a - m)))
-  if hasattr(pb, 'models'):   # probayes_amd: the same density as a descriptor
-    logp = pb.models.GaussianMixtureLogPDF(['x', 'y'], params['w'], mu, sd)
   process.set_prob(logp, pscale='log')
   process.set_tran(lambda **kw: 1.)
   step = params['step']

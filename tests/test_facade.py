@@ -249,3 +249,51 @@ def test_consecutive_samplers_continue_the_cycle():
       summary = process(process.walk(process.sampler(init, stop=stop, **kwds)))
       got.append(np.stack([np.asarray(summary.v[k]) for k in keys], -1))
     assert _golden_rtol(np.concatenate(got), g['v_x'][c]) <= 1e-12
+
+
+def test_mixture_densities_trace_or_fail_loudly():
+  """The H5 mixture written with NumPy (gmm2's own logp) lowers to the gmm
+  form; scipy.special.logsumexp is the same form; anything else is
+  NotLowerable."""
+  import scipy.special
+  import scipy.stats
+  x = pb.RV('x', vtype=float, vset=(-np.inf, np.inf))
+  y = pb.RV('y', vtype=float, vset=(-np.inf, np.inf))
+  process = pb.SP(x & y)
+  process.set_tran(lambda **kw: 1.)
+  process.set_delta(lambda: process.Delta(x=scipy.stats.norm.rvs(scale=.5),
+                                          y=scipy.stats.norm.rvs(scale=.5)))
+  process.set_scores('hastings')
+  logw, mu, sd = np.log([0.4, 0.6]), np.array([[0., 1.], [2., -1.]]), \
+      np.array([0.5, 0.7])
+
+  def lse(**kw):
+    a = logw + scipy.stats.norm.logpdf(kw['x'], mu[:, 0], sd) + \
+        scipy.stats.norm.logpdf(kw['y'], mu[:, 1], sd)
+    return scipy.special.logsumexp(a)
+  process.set_prob(lse, pscale='log')
+  tg = process.lower()['target']
+  assert tg['kind'] == 'gmm'
+  np.testing.assert_array_equal(tg['mu'], mu)
+  np.testing.assert_array_equal(tg['logw'], logw)
+
+  def bad_sd(**kw):
+    a = logw + scipy.stats.norm.logpdf(kw['x'], mu[:, 0], sd) + \
+        scipy.stats.norm.logpdf(kw['y'], mu[:, 1], 2 * sd)
+    m = np.max(a)
+    return m + np.log(np.sum(np.exp(a - m)))
+
+  def no_shift(**kw):
+    a = logw + scipy.stats.norm.logpdf(kw['x'], mu[:, 0], sd) + \
+        scipy.stats.norm.logpdf(kw['y'], mu[:, 1], sd)
+    return np.log(np.sum(np.exp(a)))
+
+  def swapped(**kw):
+    a = logw + scipy.stats.norm.logpdf(kw['y'], mu[:, 1], sd) + \
+        scipy.stats.norm.logpdf(kw['x'], mu[:, 0], sd)
+    m = np.max(a)
+    return m + np.log(np.sum(np.exp(a - m)))
+  for fn in (bad_sd, no_shift, swapped):
+    process.set_prob(fn, pscale='log')
+    with pytest.raises(pb.NotLowerable):
+      process.lower()

@@ -51,8 +51,13 @@ def test_production_law_matches_oracle(name, mode):
         assert np.array_equal(np.unique(a[:, k]), np.unique(b[:, k]))
         continue
       assert abs(a[:, k].mean() - b[:, k].mean()) <= 5 * se, (step, k)
-      assert abs(sa / sb - 1) <= 5 * np.sqrt(0.5 / n_cpu + 0.5 / n_gpu) + 0.02, \
-          (step, k, sa, sb)
+      # variances, with the sampling error of s^2 from the fourth moment
+      # (the state laws are skewed and discrete near fixed steps / limits)
+      va, vb = sa ** 2, sb ** 2
+      m4a = np.mean((a[:, k] - a[:, k].mean()) ** 4)
+      m4b = np.mean((b[:, k] - b[:, k].mean()) ** 4)
+      se_v = np.sqrt((m4a - va ** 2) / n_gpu + (m4b - vb ** 2) / n_cpu)
+      assert abs(va - vb) <= 5 * se_v + 1e-12 * vb, (step, k, va, vb)
   pa, pb = g['u'].mean(), r['u'].mean()
   assert abs(pa - pb) <= 5 * np.sqrt(pb * (1 - pb) / (n_cpu * t)) + 1e-3
 

@@ -156,9 +156,33 @@ def test_facade_lowers_the_descriptor_and_refuses_other_tfuns(root):
   assert spec['kind'] == 'linreg' and spec['names'] == list(linreg.KEYS)
   assert spec['vsets'] == [(-6., 6.), (-6., 6.), (0.001, 10.)]
   assert process.lower(extra, iid=True, joint=False)['vsets'] is None
-  process2, _, extra2, _, _, _, _ = _facade(root)      # a closure cond_reg
-  with pytest.raises(pb.NotLowerable):
-    process2.lower(extra2, iid=True, joint=True)
+  # the example's own closure cond_reg: identified by probing
+  process2, _, extra2, _, _, _, _ = _facade(root)
+  spec2 = process2.lower(extra2, iid=True, joint=True)
+  assert spec2['kind'] == 'linreg' and spec2['hyper'] == (0., 1., 0., 1., 1., 1.)
+  from mcmc_examples import linreg_cond
+  x, y = spec2['x_obs'], spec2['y_obs']
+
+  def wrong_scale(x, y, beta_0, beta_1, y_sigma, unknown):
+    if unknown == 'beta_1':      # variance passed where NumPy wants the sd
+      y_prec = 1 / y_sigma ** 2
+      cond_var = 1 / (1. + y_prec * np.sum(x ** 2))
+      return np.random.normal(cond_var * y_prec * np.sum(x * (y - beta_0)),
+                              cond_var)
+    return linreg_cond(x, y)(x, y, beta_0, beta_1, y_sigma, unknown)
+
+  def two_draws(x, y, beta_0, beta_1, y_sigma, unknown):
+    np.random.normal()
+    return linreg_cond(x, y)(x, y, beta_0, beta_1, y_sigma, unknown)
+
+  def other_hyper(x, y, beta_0, beta_1, y_sigma, unknown):
+    return linreg_cond(x, y)(x, y, beta_0, beta_1, y_sigma, unknown,
+                             beta_0_mu=0.25, y_sigma_beta=2.)
+  for fn in (wrong_scale, two_draws):
+    with pytest.raises(pb.NotLowerable):
+      linreg.identify_conditional(fn, x, y)
+  assert linreg.identify_conditional(other_hyper, x, y) == \
+      (0.25, 1., 0., 1., 1., 2.)
   process.set_prob(lambda x, y, beta_0, beta_1, y_sigma: -(y - beta_0) ** 2,
                    pscale='log')
   with pytest.raises(pb.NotLowerable):
@@ -170,8 +194,7 @@ def test_example_script_reproduces_reference_chain(root):
   """np.random.seed(s); sampler; walk; SP(samples) as gibbs_linreg.py:74-78
   does, on NumPy's global stream."""
   for c in range(2):
-    process, init, extra, kwds, keys, g, t = _facade(
-        root, linreg.LinRegConditional)
+    process, init, extra, kwds, keys, g, t = _facade(root)   # own cond_reg
     seed = int(g['seeds'][c])
     np.random.seed(seed)
     samples = process.walk(process.sampler(init, extra, stop=t, **kwds))
@@ -191,7 +214,7 @@ def test_example_script_reproduces_reference_chain(root):
 
 @pytest.mark.gpu
 def test_batched_sampler_reproduces_all_reference_chains(root):
-  process, init, extra, kwds, keys, g, t = _facade(root, linreg.LinRegConditional)
+  process, init, extra, kwds, keys, g, t = _facade(root)   # own cond_reg
   n = len(g['seeds'])
   sm = process.sampler(init, extra, stop=t, chains=n, seeds=g['seeds'], **kwds)
   summary = process(process.walk(sm))
@@ -259,7 +282,6 @@ def test_consecutive_samplers_continue_the_cycle(root):
   from mcmc_examples import TFUN_WORKLOADS
   g = np.load(os.path.join(root, 'tests/golden/gibbs_linreg_seg.npz'))
   builder, params = TFUN_WORKLOADS['gibbs_linreg'][:2]
-  params = dict(params, cond=linreg.LinRegConditional)
   for c in range(len(g['seeds'])):
     process, init, extra, kwds, keys = builder(pb, params)
     np.random.seed(int(g['seeds'][c]))
