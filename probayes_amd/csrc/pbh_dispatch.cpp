@@ -9,6 +9,12 @@
 
 namespace pbh {
 
+LaunchEvents &launch_events() {
+  static thread_local LaunchEvents ev;
+  return ev;
+}
+
+
 template <int D>
 hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds);
 template <int D>

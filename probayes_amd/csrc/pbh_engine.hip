@@ -63,6 +63,11 @@ struct pbh_engine {
   double *bm64 = nullptr;
   double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
   bool spin_sync = true;     // PBH_SYNC=block: hipStreamSynchronize instead
+  // timing events as marker packets around the launches (default), or
+  // PBH_EVENT_MARKERS=0: on the first / last dispatch packet
+  // (hipExtLaunchKernel: 2 us less GPU time, 3-4 us more host enqueue and
+  // ~7 us more wall per short launch, measured: profiles/r02j_events.jsonl)
+  bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
   bool gibbs_fast = true;    // PBH_GIBBS_FAST=0 keeps the ndtri kernel for Philox
@@ -187,6 +192,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gl = std::getenv("PBH_GIBBS_LANES")) e->gibbs_lanes = std::atoi(gl);
   if (const char *ml = std::getenv("PBH_GMM_LANES")) e->gmm_lanes = std::atoi(ml);
   if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
+  if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -861,10 +867,20 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
                       k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
                          ? (size_t)k.tn * sizeof(double) : 0;
-  HIP_TRY(hipEventRecord(e->ev0, e->stream));
+  // the timed region: events on the first / last dispatch packet, or (with
+  // PBH_EVENT_MARKERS=1) separate marker packets around the launches
+  pbh::LaunchEvents &lev = pbh::launch_events();
+  if (e->event_markers) {
+    HIP_TRY(hipEventRecord(e->ev0, e->stream));
+    lev = {};
+  } else {
+    lev.start = e->ev0;
+    lev.stop = nullptr;
+  }
   int64_t launches = 0;
   for (int64_t done = 0; done < n_steps;) {
     const int64_t m = std::min(spl, n_steps - done);
+    if (!e->event_markers && done + m >= n_steps) lev.stop = e->ev1;
     k.n_steps = (int32_t)m;
     k.g0 = e->g;
     k.has_pred = e->has_pred ? 1 : 0;
@@ -872,15 +888,18 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     k.gq_init = e->gq_valid ? 0 : 1;
     hipError_t err = e->has_gibbs ? pbh::launch_gibbs(k, e->stream)
                                   : pbh::launch_mh(k, e->stream, lds);
-    if (err != hipSuccess)
+    if (err != hipSuccess) {
+      lev = {};
       return fail(PBH_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(err));
+    }
     e->g += m;
     e->has_pred = true;
     e->gq_valid = gfast;   // only the production Gibbs kernel maintains g, Q
     done += m;
     ++launches;
   }
-  HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  lev = {};
+  if (e->event_markers) HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->mom_steps += n_steps;
   e->timed = true;
   e->last_launches = launches;

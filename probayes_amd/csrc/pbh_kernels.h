@@ -4,9 +4,30 @@
 // wave-uniform address (scalar loads).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace pbh {
+
+// Dispatch timing of pbh_run's timed region: the start / stop events ride on
+// the first / last kernel dispatch packet itself (hipExtLaunchKernel), so the
+// queue carries no extra event-marker packets between the host's launch and
+// the kernel.  pbh_run sets them; every MH / Gibbs launch goes through
+// pbh_launch, which consumes the start event on the first dispatch.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents &launch_events();   // thread-local (pbh_dispatch.cpp)
+
+template <typename F, typename... Args>
+inline void pbh_launch(F kernel, const dim3 &grid, const dim3 &block,
+                       size_t shm, hipStream_t st, Args... args) {
+  LaunchEvents &ev = launch_events();
+  hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, st, ev.start,
+                        ev.stop, 0u, args...);
+  ev.start = nullptr;
+}
+
 
 struct KArgs {
   // ---- model (pbh_model) ----

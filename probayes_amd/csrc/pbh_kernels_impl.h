@@ -2148,31 +2148,31 @@ template <int D, int TGT, int PROP>
 void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
   const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
   if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_REPLAY, TGT, PROP>), grid, block,
+    pbh_launch((mh_kernel<D, PBH_RNG_REPLAY, TGT, PROP>), grid, block,
                        lds, st, a);
   else if (a.rng == PBH_RNG_PHILOX)
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX, TGT, PROP>), grid, block,
+    pbh_launch((mh_kernel<D, PBH_RNG_PHILOX, TGT, PROP>), grid, block,
                        lds, st, a);
   else if (a.rng == PBH_RNG_XOSHIRO)
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_XOSHIRO, TGT, PROP>), grid, block,
+    pbh_launch((mh_kernel<D, PBH_RNG_XOSHIRO, TGT, PROP>), grid, block,
                        lds, st, a);
   else
-    hipLaunchKernelGGL((mh_kernel<D, PBH_RNG_PHILOX_F64, TGT, PROP>), grid,
+    pbh_launch((mh_kernel<D, PBH_RNG_PHILOX_F64, TGT, PROP>), grid,
                        block, lds, st, a);
 }
 
 template <int D, bool MOM>
 void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
   if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_REPLAY, MOM>), grid, block, 0, st, a);
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_REPLAY, MOM>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_PHILOX)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX, MOM>), grid, block, 0, st, a);
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX, MOM>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_XOSHIRO)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_XOSHIRO, MOM>), grid, block, 0, st, a);
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_XOSHIRO, MOM>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_PHILOX_FP32)
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_FP32, MOM>), grid, block, 0, st, a);
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX_FP32, MOM>), grid, block, 0, st, a);
   else
-    hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX_F64, MOM>), grid, block, 0, st, a);
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX_F64, MOM>), grid, block, 0, st, a);
 }
 
 template <int D>
@@ -2227,25 +2227,25 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
         const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
         if (L == 2) {
           if (a.tn == 2)
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 2, 2>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_lanes_kernel<D, 2, 2>), grid, block, 0, st, a);
           else if (a.tn == 3)
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 3, 2>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_lanes_kernel<D, 3, 2>), grid, block, 0, st, a);
           else
-            hipLaunchKernelGGL((mh_gmm_lanes_kernel<D, 4, 2>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_lanes_kernel<D, 4, 2>), grid, block, 0, st, a);
         } else if (a.moments) {
           if (a.tn == 2)
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 2, true>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 2, true>), grid, block, 0, st, a);
           else if (a.tn == 3)
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 3, true>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 3, true>), grid, block, 0, st, a);
           else
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 4, true>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 4, true>), grid, block, 0, st, a);
         } else {
           if (a.tn == 2)
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 2, false>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 2, false>), grid, block, 0, st, a);
           else if (a.tn == 3)
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 3, false>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 3, false>), grid, block, 0, st, a);
           else
-            hipLaunchKernelGGL((mh_gmm_quad_kernel<D, 4, false>), grid, block, 0, st, a);
+            pbh_launch((mh_gmm_quad_kernel<D, 4, false>), grid, block, 0, st, a);
         }
         return hipGetLastError();
       }
@@ -2275,17 +2275,17 @@ hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
     const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
     if constexpr (D % 4 == 0) {
       if (L == 4) {
-        hipLaunchKernelGGL((gibbs_fast_kernel<D, 4>), grid, block, 0, st, a);
+        pbh_launch((gibbs_fast_kernel<D, 4>), grid, block, 0, st, a);
         return hipGetLastError();
       }
     }
     if constexpr (D % 2 == 0) {
       if (L == 2) {
-        hipLaunchKernelGGL((gibbs_fast_kernel<D, 2>), grid, block, 0, st, a);
+        pbh_launch((gibbs_fast_kernel<D, 2>), grid, block, 0, st, a);
         return hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((gibbs_fast_kernel<D, 1>), grid, block, 0, st, a);
+    pbh_launch((gibbs_fast_kernel<D, 1>), grid, block, 0, st, a);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
@@ -2293,25 +2293,25 @@ hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
     if (a.gibbs_mfma) {
       const size_t lds = (kBlock / 64) * 64 * MvnMfma<D>::S * sizeof(double);
       if (a.rng == PBH_RNG_REPLAY)
-        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, true>), grid, block,
+        pbh_launch((gibbs_kernel<D, PBH_RNG_REPLAY, true>), grid, block,
                            lds, st, a);
       else if (a.rng == PBH_RNG_XOSHIRO)
-        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_XOSHIRO, true>), grid, block,
+        pbh_launch((gibbs_kernel<D, PBH_RNG_XOSHIRO, true>), grid, block,
                            lds, st, a);
       else
-        hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, true>), grid, block,
+        pbh_launch((gibbs_kernel<D, PBH_RNG_PHILOX, true>), grid, block,
                            lds, st, a);
       return hipGetLastError();
     }
   }
   if (a.rng == PBH_RNG_REPLAY)
-    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_REPLAY, false>), grid, block, 0,
+    pbh_launch((gibbs_kernel<D, PBH_RNG_REPLAY, false>), grid, block, 0,
                        st, a);
   else if (a.rng == PBH_RNG_XOSHIRO)
-    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_XOSHIRO, false>), grid, block, 0,
+    pbh_launch((gibbs_kernel<D, PBH_RNG_XOSHIRO, false>), grid, block, 0,
                        st, a);
   else
-    hipLaunchKernelGGL((gibbs_kernel<D, PBH_RNG_PHILOX, false>), grid, block, 0,
+    pbh_launch((gibbs_kernel<D, PBH_RNG_PHILOX, false>), grid, block, 0,
                        st, a);
   return hipGetLastError();
 }

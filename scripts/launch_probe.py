@@ -42,7 +42,8 @@ def probe(rng, moments, steps, reps, sync_env, trace=True, chains=65536,
     kern.append(eng.last_run_ms()[0] / 1e3)
   eng.close()
   med = lambda v: float(np.median(v))
-  out = {'rng': rng, 'moments': moments, 'steps': steps, 'sync': sync_env or 'spin',
+  out = {'rng': rng, 'moments': moments, 'steps': steps, 'chains': chains,
+         'sync': sync_env or 'spin',
          'trace': trace, 'spl': spl, 'wall_us': med(walls) * 1e6,
          'enqueue_us': med(enq) * 1e6, 'kernel_us': med(kern) * 1e6,
          'value_wall': chains * steps / med(walls),
