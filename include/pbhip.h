@@ -256,10 +256,18 @@ int pbh_trace_ess(pbh_engine *eng, int64_t first, int64_t count, double *ess);
  * [first, first + count) (PD summate + expectation over a recorded trace,
  * pd_utils.py:332-411, pd.py:373-407, without copying the trace to the
  * host).  The result replaces the engine's moment buffers (what
- * pbh_rccl_allgather_moments sends, n_steps = count); host pointers may be
+ * pbh_rccl_allgather_stats sends, n_steps = count); host pointers may be
  * NULL.                                                                     */
 int pbh_trace_stats(pbh_engine *eng, int64_t first, int64_t count, double *sum,
                     double *sumsq, int64_t *n_acc);
+/* PD.expectation of a summary over trace records [first, first + count) on
+ * the device (pd.py:373-405): per chain and dim sum_t p_t v_t^e /
+ * max(tiny, sum_t p_t), p_t = v.prob rescaled to linear (exp_logp of the
+ * recorded log-prob under a log pscale), v^e = v when exponent is 0 (the
+ * reference's `val ** exponent if exponent else val`), sums in record
+ * order.  out [d][N] on the host.                                           */
+int pbh_trace_expectation(pbh_engine *eng, int64_t first, int64_t count,
+                          double exponent, double *out);
 
 /* ---- multi-GPU: one RCCL all-gather over xGMI --------- */
 int pbh_rccl_unique_id(uint8_t id[128]);

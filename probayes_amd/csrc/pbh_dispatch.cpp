@@ -164,6 +164,45 @@ hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
   return hipGetLastError();
 }
 
+// PD.expectation over trace records [first, first + count): thread (k, c)
+// walks chain c's column of dim k and its log-probs in record order --
+// NumPy's axis-0 sums are sequential per column, and prob * v is rounded
+// before the add, as here (no contraction in this file's build).
+__global__ void trace_expect_kernel(const double *tx, const double *tlp,
+                                    int64_t n, int32_t d, int64_t first,
+                                    int64_t count, double exponent, int32_t lin,
+                                    double log_npi, double *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = i / n, c = i % n;
+  if (k >= d) return;
+  const double *xv = tx + (first * d + k) * n + c;
+  const double *lv = tlp + first * n + c;
+  double sp = 0., spv = 0.;
+  for (int64_t r = 0; r < count; ++r, xv += d * n, lv += n) {
+    const double l = *lv;
+    const double p = lin ? l : (l <= log_npi ? exp(l) : 1.7976931348623158e+308);
+    double v = *xv;
+    if (exponent == 2.0) v = v * v;                    // NumPy's square loop
+    else if (exponent != 0.0 && exponent != 1.0) v = pow(v, exponent);
+    sp = sp + p;
+    spv = spv + p * v;
+  }
+  const double tiny = 2.2250738585072014e-308;       // NEARLY_POSITIVE_ZERO
+  const double den = sp != sp ? sp : (sp > tiny ? sp : tiny);
+  out[k * n + c] = spv / den;
+}
+
+hipError_t launch_trace_expectation(const double *tx, const double *tlp,
+                                    int64_t n, int32_t d, int64_t first,
+                                    int64_t count, double exponent, int32_t lin,
+                                    double log_npi, double *out, hipStream_t s) {
+  const int64_t m = (int64_t)d * n;
+  hipLaunchKernelGGL(trace_expect_kernel, dim3((unsigned)((m + 255) / 256)),
+                     dim3(256), 0, s, tx, tlp, n, d, first, count, exponent,
+                     lin, log_npi, out);
+  return hipGetLastError();
+}
+
 // Effective sample size of every (chain, dim) series of trace records
 // [first, first + count): Geyer's initial positive sequence on the
 // autocorrelations of the centred series, the estimator of

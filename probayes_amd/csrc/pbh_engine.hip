@@ -67,6 +67,7 @@ struct pbh_engine {
   // PBH_EVENT_MARKERS=0: on the first / last dispatch packet
   // (hipExtLaunchKernel: 2 us less GPU time, 3-4 us more host enqueue and
   // ~7 us more wall per short launch, measured: profiles/r02j_events.jsonl)
+  bool gmm_full = true;      // PBH_GMM_FULL=0: no steady-state quad kernel
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -193,6 +194,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *ml = std::getenv("PBH_GMM_LANES")) e->gmm_lanes = std::atoi(ml);
   if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
+  if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -859,6 +861,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gibbs_fast = e->gibbs_fast ? 1 : 0;
   k.gibbs_lanes = e->gibbs_lanes;
   k.gmm_lanes = e->gmm_lanes;
+  k.gmm_full = e->gmm_full ? 1 : 0;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;
@@ -1027,6 +1030,31 @@ int pbh_trace_stats(pbh_engine *e, int64_t first, int64_t count, double *sum,
   if (sum) HIP_TRY(hipMemcpy(sum, e->msum, dn * sizeof(double), hipMemcpyDeviceToHost));
   if (sumsq) HIP_TRY(hipMemcpy(sumsq, e->msq, dn * sizeof(double), hipMemcpyDeviceToHost));
   if (n_acc) HIP_TRY(hipMemcpy(n_acc, e->nacc, n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_trace_expectation(pbh_engine *e, int64_t first, int64_t count,
+                          double exponent, double *out) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  int64_t rec = 0;
+  pbh_trace_len(e, &rec);
+  if (first < 0 || count < 1 || first + count > rec)
+    return fail(PBH_ERR_ARG, "trace range [%lld, %lld) outside [0, %lld)",
+                (long long)first, (long long)(first + count), (long long)rec);
+  if (!std::isfinite(exponent)) return fail(PBH_ERR_ARG, "exponent must be finite");
+  HIP_TRY(hipSetDevice(e->device));
+  const size_t dn = (size_t)e->d * e->n;
+  double *dout = nullptr;
+  HIP_TRY(hipMalloc(&dout, dn * sizeof(double)));
+  hipError_t err = pbh::launch_trace_expectation(
+      e->tx, e->tlp, e->n, e->d, first, count, exponent,
+      e->k.pscale == PBH_PSCALE_LIN ? 1 : 0, e->k.log_npi, dout, e->stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+  if (err == hipSuccess)
+    err = hipMemcpy(out, dout, dn * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(dout);
+  if (err != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_trace_expectation: %s", hipGetErrorString(err));
   return PBH_OK;
 }
 

@@ -100,6 +100,7 @@ struct KArgs {
   int32_t gq_init;     // 1: recompute g, Q from x at entry
   int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
   int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
+  int32_t gmm_full;    // the quad kernel's steady-state form is allowed
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;
@@ -131,6 +132,10 @@ hipError_t launch_trace_stats(const double *tx, const uint64_t *tacc, int64_t n,
                               int64_t count, double *sum, double *sumsq,
                               int64_t *nacc, hipStream_t s);
 // per-(chain, dim) initial-positive-sequence ESS of trace records
+hipError_t launch_trace_expectation(const double *tx, const double *tlp,
+                                    int64_t n, int32_t d, int64_t first,
+                                    int64_t count, double exponent, int32_t lin,
+                                    double log_npi, double *out, hipStream_t s);
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
                             hipStream_t st);

@@ -1414,7 +1414,27 @@ __device__ __forceinline__ float qperm_f32(float v) {
                                        __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
 
-template <int D, int K, bool MOM>
+// The rare undecided step of the quad kernel (accept_filter_ms32's need):
+// the exact ratio form of (lp', lp) on t's full 53 bits, out of line so that
+// the steady-state loop keeps neither its registers nor its code.
+__device__ __attribute__((noinline)) bool gmm_quad_exact(
+    const KArgs &a, const double *tab, int64_t g, int64_t chain, uint32_t lead,
+    double M, double S, double lm, double ls, double lp0) {
+  constexpr int LB = 14;
+  const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+  const double t = u01((lead << (32 - LB)) | (w.x >> LB), w.y);
+  const double lpp = M + ln_tab(S, tab);
+  const double lpc = lm == lp0 && ls == 1.0 ? lp0 : lm + ln_tab(ls, tab);
+  return ratio_accept(lpp * a.acc_beta, lpc * a.acc_beta, t, false, a.log_npi);
+}
+
+// FULL: the steady-state launch (gmm_quad_full): whole groups of 4 steps,
+// every step recorded (thin 1, inside the trace), the chains past step 1 and
+// the plain ratio form (acc_beta = 1) -- no per-step range, record or
+// first-step tests, and branch-free stores: a lane with nothing of its own
+// to write (a part p >= D, or a padding chain, which runs chain 0's exact
+// trajectory) rewrites the identical value of a lane that has.
+template <int D, int K, bool MOM, bool FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_gmm_quad_kernel(KArgs a) {
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
@@ -1452,7 +1472,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   int64_t nacc = 0;
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
-  const uint32_t xoff = (uint32_t)(((int64_t)(p < D ? p : 0) * a.n + cc) * 8);
+  const uint32_t xoff = (uint32_t)(((int64_t)(p % D) * a.n + cc) * 8);
   double *txrow = a.tx + ri * D * a.n;   // record ri's rows (wave-uniform)
   const int64_t rstride = (int64_t)D * a.n;
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
@@ -1484,7 +1504,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       grec[j] = -1;
       gm[j] = lm;
       gs[j] = ls;
-      if (g < a.g0 || g >= gend) return;   // wave-uniform
+      if (!FULL && (g < a.g0 || g >= gend)) return;   // wave-uniform
       const int s = (int)(g - a.g0);
       double xp[D];
 #pragma unroll
@@ -1507,7 +1527,13 @@ void mh_gmm_quad_kernel(KArgs a) {
       e = e + qperm_f64<kQuadXor1>(e);
       const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
       bool acc;
-      if (!a.has_pred && s == 0) {
+      if constexpr (FULL) {
+        const Decision dc = accept_filter_ms32<LB>(M, S32, lm, ls32, lead);
+        acc = dc.acc;
+        if (__ballot(dc.need)) {   // wave-uniform, rare
+          if (dc.need) acc = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
+        }
+      } else if (!a.has_pred && s == 0) {
         acc = true;                                  // s = None on step 1
       } else {
         const Decision dc = a.acc_beta == 1.0
@@ -1540,6 +1566,23 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
         ms += xo;
         mq = __builtin_fma(xo, xo, mq);
+      }
+      if constexpr (FULL) {
+        double xo = x[0];
+#pragma unroll
+        for (int i = 1; i < D; ++i) xo = p % D == i ? x[i] : xo;
+        st_buf(txrow, xoff, 0, xo);
+        grec[j] = ri;
+        uint64_t m = __ballot(acc) & 0x1111111111111111ull & act_bits;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0xFFFFull;
+        // every lane stores the wave's word (one address, one value)
+        reinterpret_cast<uint16_t *>(a.tacc)[ri * 4 * a.W + wave] = (uint16_t)m;
+        ++ri;
+        txrow += rstride;
+        return;
       }
       const bool rec_now = ph == 0;
       const int64_t rec = ri;
@@ -1581,9 +1624,9 @@ void mh_gmm_quad_kernel(KArgs a) {
       pss = p == j ? gs[j] : pss;
       prec = p == j ? grec[j] : prec;
     }
-    if (prec >= 0 && active) {
+    if (FULL || (prec >= 0 && active)) {
       const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
-      __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + c]);
+      __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + cc]);
     }
   }
   if (active) {
@@ -2202,6 +2245,26 @@ inline bool gmm_pair_form(const KArgs &a) {
          a.d * a.n * 8 < (int64_t(1) << 32);   // 32-bit trace byte offsets
 }
 
+// The quad kernel's steady-state form applies (see mh_gmm_quad_kernel FULL):
+// whole 4-step groups, thin 1, every record inside the trace, past step 1,
+// acc_beta = 1.  PBH_GMM_FULL=0 (engine: gmm_full) keeps the general form.
+inline bool gmm_quad_full(const KArgs &a) {
+  return a.gmm_full && a.has_pred && a.acc_beta == 1.0 && a.thin == 1 &&
+         a.tx != nullptr && a.g0 % 4 == 0 && a.n_steps % 4 == 0 &&
+         a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
+}
+
+template <int D, bool MOM, bool FULL>
+void launch_gmm_quad(const KArgs &a, const dim3 &grid, const dim3 &block,
+                     hipStream_t st) {
+  if (a.tn == 2)
+    pbh_launch((mh_gmm_quad_kernel<D, 2, MOM, FULL>), grid, block, 0, st, a);
+  else if (a.tn == 3)
+    pbh_launch((mh_gmm_quad_kernel<D, 3, MOM, FULL>), grid, block, 0, st, a);
+  else
+    pbh_launch((mh_gmm_quad_kernel<D, 4, MOM, FULL>), grid, block, 0, st, a);
+}
+
 template <int D>
 hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
   if constexpr (D % 2 == 0 && D >= 4) {
@@ -2232,20 +2295,15 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
             pbh_launch((mh_gmm_lanes_kernel<D, 3, 2>), grid, block, 0, st, a);
           else
             pbh_launch((mh_gmm_lanes_kernel<D, 4, 2>), grid, block, 0, st, a);
+        } else if (gmm_quad_full(a)) {
+          if (a.moments)
+            launch_gmm_quad<D, true, true>(a, grid, block, st);
+          else
+            launch_gmm_quad<D, false, true>(a, grid, block, st);
         } else if (a.moments) {
-          if (a.tn == 2)
-            pbh_launch((mh_gmm_quad_kernel<D, 2, true>), grid, block, 0, st, a);
-          else if (a.tn == 3)
-            pbh_launch((mh_gmm_quad_kernel<D, 3, true>), grid, block, 0, st, a);
-          else
-            pbh_launch((mh_gmm_quad_kernel<D, 4, true>), grid, block, 0, st, a);
+          launch_gmm_quad<D, true, false>(a, grid, block, st);
         } else {
-          if (a.tn == 2)
-            pbh_launch((mh_gmm_quad_kernel<D, 2, false>), grid, block, 0, st, a);
-          else if (a.tn == 3)
-            pbh_launch((mh_gmm_quad_kernel<D, 3, false>), grid, block, 0, st, a);
-          else
-            pbh_launch((mh_gmm_quad_kernel<D, 4, false>), grid, block, 0, st, a);
+          launch_gmm_quad<D, false, false>(a, grid, block, st);
         }
         return hipGetLastError();
       }

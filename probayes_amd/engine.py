@@ -377,6 +377,17 @@ class Engine:
               _c.c_int64(int(count)), _dp(out))
     return out.T.copy()
 
+  def trace_expectation(self, first=0, count=None, exponent=None):
+    """PD.expectation (pd.py:373-405) of the summary of trace records
+    [first, first + count), computed on the device: [N, d] of
+    sum p v^exponent / sum p with p the recorded prob rescaled to linear."""
+    count = self.trace_len() - first if count is None else count
+    out = np.empty((self.dim, self.n))
+    _lib.call('pbh_trace_expectation', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(count)), _c.c_double(float(exponent or 0.)),
+              _dp(out))
+    return out.T.copy()
+
   def rccl_allreduce_max(self, value):
     v = _c.c_double(float(value))
     _lib.call('pbh_rccl_allreduce_max', self._h, _c.byref(v))

@@ -59,6 +59,66 @@ def _quantile_1d(vals, prob, pscale, quants):
   return out
 
 
+def _interp2(x, c0, c1, v0, v1):
+  """np.interp(x, [c0, c1], [v0, v1]) elementwise, NumPy's own arithmetic
+  (numpy/_core/src/multiarray/compiled_base.c arr_interp): below -> v0,
+  above or at c1 -> v1, at c0 -> v0, else slope (x - c0) + v0 with the
+  NaN fallbacks."""
+  with np.errstate(divide='ignore', invalid='ignore'):
+    slope = (v1 - v0) / (c1 - c0)
+    mid = slope * (x - c0) + v0
+    alt = slope * (x - c1) + v1
+    mid = np.where(np.isnan(mid), np.where(np.isnan(alt) & (v0 == v1), v0, alt),
+                   mid)
+  out = np.where(x == c0, v0, mid)
+  out = np.where(x >= c1, v1, out)
+  return np.where(x < c0, v0, out)
+
+
+def _quantile_batched(vals, prob, pscale, quants):
+  """_quantile_1d for every chain of [T, N] summaries at once (the same
+  operations, vectorised over the chain axis): one dict per quantile per
+  chain, as the per-chain loop returns."""
+  prob = np.asarray(prob, float)
+  T, N = prob.shape
+  ravprob = rescale(prob, pscale, 'lin')
+  cumprob = np.cumsum(ravprob, axis=0)
+  cumprob = _div_prob(cumprob, cumprob[-1])
+  cols = np.arange(N)
+  per_q = []
+  for q in quants:
+    # np.digitize(q, cumprob) on non-decreasing bins = #{bins <= q}
+    ridx = np.maximum(0, np.sum(cumprob <= q, axis=0) - 1)
+    res = {}
+    for key, v in vals.items():
+      v = np.asarray(v).reshape(T, N)
+      if T > 1:
+        d = v[1:] >= v[:-1]
+        mono = d.all(axis=0) | (~d).all(axis=0)
+      else:
+        mono = np.ones(N, bool)
+      idx = np.minimum(ridx, T - 1)
+      last = idx == T - 1
+      i1 = np.minimum(idx + 1, T - 1)
+      v0, v1 = v[idx, cols], v[i1, cols]
+      p0, p1 = ravprob[idx, cols], ravprob[i1, cols]
+      c0, c1 = cumprob[idx, cols], cumprob[i1, cols]
+      near = np.abs(p1 - p0) < min(q, 1. - q)
+      with np.errstate(divide='ignore', invalid='ignore'):
+        weighted = (p0 * v0 + p1 * v1) / (p0 + p1)
+      got = np.where(last, v0, np.where(near, _interp2(q, c0, c1, v0, v1),
+                                        weighted))
+      res[key] = (got, mono)
+    per_q.append(res)
+  out = []
+  for c in range(N):
+    chain = []
+    for res in per_q:
+      chain.append({k: (g[c] if m[c] else {T}) for k, (g, m) in res.items()})
+    out.append(chain)
+  return out
+
+
 class PD(dict):
   """Named dict of arrays with .prob and .pscale (pd.py:15-45)."""
 
@@ -116,12 +176,8 @@ class PD(dict):
     if prob.ndim <= 1:
       res = _quantile_1d(dict(self), prob, self.pscale, quants)
       return res[0] if scalar else res
-    per_chain = []
-    for c in range(prob.shape[1]):
-      vals = {k: np.asarray(v)[:, c] for k, v in self.items()}
-      res = _quantile_1d(vals, prob[:, c], self.pscale, quants)
-      per_chain.append(res[0] if scalar else res)
-    return per_chain
+    res = _quantile_batched(dict(self), prob, self.pscale, quants)
+    return [r[0] if scalar else r for r in res]
 
   def marginal(self, keys):
     """pd.py:168-211 for a summary, whose variables share the sample axis:

@@ -400,6 +400,34 @@ def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch, lanes):
   np.testing.assert_allclose(mp['sum'], m1['sum'], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize('mom', [True, False])
+def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
+  """The quad kernel's steady-state launch (whole 4-step groups, no
+  per-step range / record tests, branch-free stores) is bit-for-bit the
+  general form (PBH_GMM_FULL=0); ragged chain count, several launches."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec('gmm2')
+  n, t = 3000 + 5, 200
+  outs = {}
+  for full in ('1', '0'):
+    monkeypatch.setenv('PBH_GMM_FULL', full)
+    eng = Engine(spec)
+    eng.init_chains(golden_init('gmm2', n))
+    eng.set_rng('philox', seed=9)
+    eng.set_collect(moments=mom)
+    eng.alloc_trace(t, 1)
+    eng.run(t, steps_per_launch=64)
+    outs[full] = (eng.trace(), eng.moments() if mom else None, eng.state())
+    eng.close()
+  (ta, ma, sa), (tb, mb, sb) = outs['1'], outs['0']
+  for k in ('v_x', 'v_p', 'u'):
+    assert np.array_equal(ta[k], tb[k]), k
+  assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+  if mom:
+    for k in ('sum', 'sumsq', 'n_acc'):
+      assert np.array_equal(ma[k], mb[k]), k
+
+
 @pytest.mark.parametrize('name,thin,spl', [('diag10', 3, 0), ('diag10', 4, 7),
                                            ('gmm2', 4, 9), ('gibbs8', 5, 13),
                                            ('gibbs_sweep2', 3, 5)])

@@ -91,3 +91,40 @@ def test_conditionalise_raises_as_reference(case):
     assert type(info.value).__name__ == err
   with pytest.raises(AssertionError):
     v.conditionalise('not_a_key')
+
+
+def test_vectorised_quantile_equals_the_per_chain_restatement():
+  """PD.quantile on [T, N] summaries runs vectorised over chains
+  (_quantile_batched); every chain's result equals _quantile_1d's (the
+  restatement pinned against the reference's recorded quantiles) bit for
+  bit: sorted and unsorted keys, ties, flat probabilities, q at 0 and 1,
+  log and linear pscales."""
+  from probayes_amd.pd import _quantile_1d
+  rs = np.random.RandomState(4)
+  T, N = 40, 37
+  x = np.sort(rs.normal(size=(T, N)), axis=0)
+  x[:, 3] = x[::-1, 3]                        # decreasing
+  x[:, 5] = rs.normal(size=T)                 # unsorted
+  x[10:14, 7] = x[10, 7]                      # ties
+  y = rs.normal(size=(T, N))
+  cases = [(rs.normal(-3, 2, (T, N)), 'log'),
+           (np.log(np.full((T, N), 0.1)), 'log'),
+           (rs.uniform(0, 1, (T, N)), 'lin')]
+  p2 = cases[2][0]
+  p2[:, 9] = 0.
+  p2[20, 9] = 1.                              # one non-zero weight
+  for prob, ps in cases:
+    pd_ = PD('p', {'x': x, 'y': y}, prob=prob, pscale=ps)
+    qs = [0., 0.1, 0.25, 0.5, 0.9, 1.]
+    got = pd_.quantile(qs)
+    for c in range(N):
+      ref = _quantile_1d({'x': x[:, c], 'y': y[:, c]}, prob[:, c], ps, qs)
+      for a, b in zip(got[c], ref):
+        for k in ('x', 'y'):
+          if isinstance(b[k], set):
+            assert a[k] == b[k]
+          else:
+            assert a[k] == b[k] or (np.isnan(a[k]) and np.isnan(b[k])), \
+                (c, k, a[k], b[k])
+    one = pd_.quantile(0.5)
+    assert all(isinstance(r, dict) for r in one)
