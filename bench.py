@@ -116,7 +116,7 @@ def measured_traffic(chains, launch_steps, rng, trace):
   launch, RNG mode), from the newest profiles/r*_traffic.json (rocprofv3 PMC
   passes, scripts/profile.sh), or None when no profile matches."""
   import glob
-  files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic.json')))
+  files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic*.json')))
   if not trace:
     return None
   for path in reversed(files):   # newest profile of this kernel and shape
