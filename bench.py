@@ -164,7 +164,9 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
       col.allreduce_max(0.0)
 
   if warmup:
-    eng.run(warmup, steps_per_launch=spl)
+    # a short warm-up runs as one-step launches, so that the dispatch path
+    # the timed launch takes has been exercised (same step count)
+    eng.run(warmup, steps_per_launch=1 if warmup <= 16 else spl)
   barrier()
   t0 = time.perf_counter()
   eng.run(steps, steps_per_launch=spl, sync=False)

@@ -784,6 +784,21 @@ int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug
     free_trace(e);
     return rc;
   }
+  if (capacity > 0) {
+    // zero-fill: unwritten records read as zeros, and every page of the
+    // trace is mapped and touched before the first run writes it (the
+    // first writes of a short run otherwise pay the translation misses)
+    const size_t dn = (size_t)capacity * d * n;
+    HIP_TRY(hipMemsetAsync(e->tx, 0, dn * sizeof(double), e->stream));
+    HIP_TRY(hipMemsetAsync(e->tlp, 0, (size_t)capacity * n * sizeof(double), e->stream));
+    HIP_TRY(hipMemsetAsync(e->tacc, 0, (size_t)capacity * W * sizeof(uint64_t), e->stream));
+    if (debug) {
+      HIP_TRY(hipMemsetAsync(e->tpx, 0, dn * sizeof(double), e->stream));
+      HIP_TRY(hipMemsetAsync(e->tpp, 0, (size_t)capacity * n * sizeof(double), e->stream));
+      HIP_TRY(hipMemsetAsync(e->ts, 0, (size_t)capacity * n * sizeof(double), e->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
   e->cap = capacity;
   e->thin = thin;
   e->debug = debug ? 1 : 0;

@@ -10,6 +10,7 @@ OUT=$R/gpurun_out/prof2
 rm -rf $OUT && mkdir -p $OUT
 cd /tmp
 for S in s20 s1000; do
+  mkdir -p $OUT/$S
   if [ $S = s20 ]; then ARGS="--steps 20 --warmup 5 --no-cpu-baseline"; else ARGS="--steps 1000 --warmup 250 --no-cpu-baseline"; fi
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$S/trace -o run -- python3 $R/bench.py $ARGS > $OUT/$S/bench_trace.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$S/fetch -o run -- python3 $R/bench.py $ARGS > $OUT/$S/bench_fetch.log 2>&1
