@@ -198,6 +198,19 @@ int pbh_init_chains(pbh_engine *eng, int64_t n_chains, int64_t chain_offset,
  * after pbh_init_chains.                                                     */
 int pbh_set_step(pbh_engine *eng, int64_t step);
 int pbh_set_rng(pbh_engine *eng, int32_t mode, uint64_t seed);
+/* Checkpoint / resume: everything a chain needs to continue
+ * exactly -- state x [N][d] and its prob lp [N], the global step index
+ * (Philox counter, CondCov cycle phase), whether step 1 is behind (the
+ * auto-accept, sp.py:231-232), and for XOSHIRO the per-chain generator
+ * state [8][N] (NULL otherwise).  pbh_restore goes after pbh_init_chains
+ * (same N) and pbh_set_rng, before pbh_alloc_trace; a run from the restored
+ * engine continues the checkpointed one step for step.  The production Gibbs
+ * kernel's persisted g, Q are recomputed from x (v.prob then agrees to its
+ * refresh tolerance, 1e-9).                                                 */
+int pbh_get_checkpoint(pbh_engine *eng, double *x, double *lp, int64_t *step,
+                       int32_t *has_pred, uint32_t *xo);
+int pbh_restore(pbh_engine *eng, const double *x, const double *lp,
+                int64_t step, int32_t has_pred, const uint32_t *xo);
 /* Replay stream [n_steps][R][n_chains] (R = d + 1 for MH, 1 for Gibbs),
  * consumed from the next pbh_run step on.                                   */
 int pbh_upload_replay(pbh_engine *eng, int64_t n_steps, const double *rand);

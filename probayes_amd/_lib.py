@@ -109,6 +109,12 @@ SIGNATURES = {
                                      ctypes.c_int32, _u8p]),
     'pbh_rccl_max_chains': (ctypes.c_int, [ctypes.c_void_p, _i64p]),
     'pbh_rccl_allgather_stats': (ctypes.c_int, [ctypes.c_void_p, _dp, _i64p]),
+    'pbh_get_checkpoint': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp,
+                                          ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_int32),
+                                          _u32p]),
+    'pbh_restore': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp, ctypes.c_int64,
+                                   ctypes.c_int32, _u32p]),
     'pbh_trace_expectation': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_double,
                                              _dp]),

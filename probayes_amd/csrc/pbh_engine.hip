@@ -982,6 +982,52 @@ int pbh_get_state(pbh_engine *e, double *x, double *logp) {
   return PBH_OK;
 }
 
+int pbh_get_checkpoint(pbh_engine *e, double *x, double *lp, int64_t *step,
+                       int32_t *has_pred, uint32_t *xo) {
+  int rc = pbh_get_state(e, x, lp);
+  if (rc) return rc;
+  if (step) *step = e->g;
+  if (has_pred) *has_pred = e->has_pred ? 1 : 0;
+  if (xo) {
+    if (e->rng != PBH_RNG_XOSHIRO || !e->xo_seeded)
+      return fail(PBH_ERR_STATE, "no xoshiro state (rng is not XOSHIRO or no run yet)");
+    HIP_TRY(hipMemcpy(xo, e->xo, (size_t)8 * e->n * sizeof(uint32_t),
+                      hipMemcpyDeviceToHost));
+  }
+  return PBH_OK;
+}
+
+int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
+                int32_t has_pred, const uint32_t *xo) {
+  if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
+    return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  if (e->cap > 0 || e->rep)
+    return fail(PBH_ERR_STATE, "pbh_restore goes before pbh_alloc_trace / replay");
+  if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
+  if (e->rng == PBH_RNG_XOSHIRO && !xo)
+    return fail(PBH_ERR_ARG, "XOSHIRO needs the generator state xo");
+  const int64_t n = e->n;
+  const int d = e->d;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  std::vector<double> xt((size_t)n * d);
+  for (int64_t c = 0; c < n; ++c)
+    for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = x[(size_t)c * d + k];
+  HIP_TRY(hipMemcpy(e->x, xt.data(), xt.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->lp, lp, n * sizeof(double), hipMemcpyHostToDevice));
+  if (xo) {
+    if (e->rng != PBH_RNG_XOSHIRO)
+      return fail(PBH_ERR_ARG, "xo given but the rng is not XOSHIRO");
+    HIP_TRY(hipMemcpy(e->xo, xo, (size_t)8 * n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    e->xo_seeded = true;
+  }
+  e->g = step;
+  e->has_pred = has_pred != 0;
+  e->gq_valid = false;   // the production Gibbs kernel recomputes g, Q from x
+  return PBH_OK;
+}
+
 int pbh_trace_len(pbh_engine *e, int64_t *n_recorded) {
   if (check_ptr(e, "engine") || check_ptr(n_recorded, "n_recorded")) return PBH_ERR_ARG;
   const int64_t r = e->cap > 0 ? e->g / e->thin - e->rec_base : 0;

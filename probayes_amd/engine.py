@@ -88,6 +88,8 @@ class Engine:
     _lib.call('pbh_create', int(device), _c.byref(self._h))
     self.device = device
     self.n = 0
+    self.chain_offset = 0
+    self._rng = 'philox'
     self._set_model()
     if self.spec['proposal']['kind'] == 'gibbs':
       self._set_gibbs()
@@ -210,6 +212,7 @@ class Engine:
   def set_rng(self, mode='philox', seed=0):
     _lib.call('pbh_set_rng', self._h, _lib.RNG[mode],
               _c.c_uint64(int(seed) & (2 ** 64 - 1)))
+    self._rng = mode
 
   def stream_width(self):
     r = _c.c_int32()
@@ -282,6 +285,33 @@ class Engine:
     lp = np.empty(self.n)
     _lib.call('pbh_get_state', self._h, _dp(x), _dp(lp))
     return x, lp
+
+  def checkpoint(self):
+    """Everything the chains need to continue exactly (pbh_get_checkpoint):
+    x [N, d], lp [N], the global step, the step-1 flag, and the xoshiro
+    generator state when that is the RNG."""
+    x = np.empty((self.n, self.dim))
+    lp = np.empty(self.n)
+    step, hp = _c.c_int64(), _c.c_int32()
+    xo = np.empty((8, self.n), np.uint32) if self._rng == 'xoshiro' else None
+    _lib.call('pbh_get_checkpoint', self._h, _dp(x), _dp(lp), _c.byref(step),
+              _c.byref(hp),
+              None if xo is None else xo.ctypes.data_as(_lib._u32p))
+    return {'x': x, 'lp': lp, 'step': step.value, 'has_pred': bool(hp.value),
+            'xo': xo, 'chain_offset': self.chain_offset}
+
+  def restore(self, ck):
+    """Resume from checkpoint() (after init_chains of the same N and set_rng
+    with the same mode and seed, before alloc_trace)."""
+    x = np.ascontiguousarray(ck['x'], np.float64)
+    lp = np.ascontiguousarray(ck['lp'], np.float64)
+    if x.shape != (self.n, self.dim) or lp.shape != (self.n,):
+      raise ValueError('checkpoint shape does not match the engine')
+    xo = ck.get('xo')
+    xo = None if xo is None else np.ascontiguousarray(xo, np.uint32)
+    _lib.call('pbh_restore', self._h, _dp(x), _dp(lp),
+              _c.c_int64(int(ck['step'])), 1 if ck['has_pred'] else 0,
+              None if xo is None else xo.ctypes.data_as(_lib._u32p))
 
   def trace_len(self):
     r = _c.c_int64()

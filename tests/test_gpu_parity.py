@@ -493,3 +493,44 @@ def test_extreme_dims_and_chain_counts_replay(d, n):
   assert np.array_equal(out['u'], ref['u'])
   assert _rel_err(out['v_x'], ref['v_x'], 1.) <= RTOL
   assert _rel_err(out['v_p'], ref['v_p']) <= RTOL
+
+
+@pytest.mark.parametrize('name,rng', [('diag10', 'philox'), ('gmm2', 'philox'),
+                                      ('metrohast_norm1d', 'philox_f64'),
+                                      ('diag10', 'xoshiro'),
+                                      ('gibbs8', 'philox')])
+def test_checkpoint_resume_continues_the_run(name, rng):
+  """pbh_get_checkpoint / pbh_restore: a fresh engine restored
+  from a checkpoint at step 40 continues the uninterrupted run step for step
+  (production Gibbs: states exact, v.prob to the O(d) refresh tolerance)."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec(name)
+  n, t, t1 = 1000 + 7, 100, 40
+
+  def engine():
+    e = Engine(spec)
+    e.init_chains(golden_init(name, n))
+    e.set_rng(rng, seed=21)
+    return e
+  full = engine()
+  full.alloc_trace(t, 1)
+  full.run(t, steps_per_launch=16)
+  ref = full.trace()
+  full.close()
+  a = engine()
+  a.run(t1, steps_per_launch=16)
+  ck = a.checkpoint()
+  a.close()
+  assert ck['step'] == t1 and ck['has_pred']
+  b = engine()
+  b.restore(ck)
+  b.alloc_trace(t - t1, 1)
+  b.run(t - t1, steps_per_launch=16)
+  got = b.trace()
+  b.close()
+  assert np.array_equal(got['v_x'], ref['v_x'][:, t1:])
+  assert np.array_equal(got['u'], ref['u'][:, t1:])
+  if spec['scores'] == 'gibbs':
+    assert _rel_err(got['v_p'], ref['v_p'][:, t1:]) <= 1e-9
+  else:
+    assert np.array_equal(got['v_p'], ref['v_p'][:, t1:])
