@@ -45,6 +45,8 @@ struct pbh_engine {
   bool xo_seeded = false;
   // legacy NumPy RandomState per chain (pbh_legacy_seed)
   uint32_t *mt_key = nullptr;
+  bool mt_db = false;          // mt_key is [2][624][n] (double-buffered)
+  bool legacy_db = true;       // PBH_LEGACY_DB=0: the in-place state
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
   // trace
@@ -195,6 +197,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
+  if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -668,7 +671,8 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   const int64_t n = e->n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  int rc = dalloc(e->mt_key, (size_t)624 * n);
+  e->mt_db = e->legacy_db;   // the state layout is fixed at seeding
+  int rc = dalloc(e->mt_key, (size_t)(e->mt_db ? 2 : 1) * 624 * n);
   if (!rc) rc = dalloc(e->mt_pos, n);
   if (!rc) rc = dalloc(e->mt_has, n);
   if (!rc) rc = dalloc(e->mt_gauss, n);
@@ -679,7 +683,7 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   hipError_t err = hipMemcpy(dseeds, seeds, n * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (err == hipSuccess)
     err = pbh::launch_legacy_seed(e->mt_key, e->mt_pos, e->mt_gauss, e->mt_has,
-                                  dseeds, n, e->stream);
+                                  dseeds, n, e->mt_db ? 1 : 0, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   dfree(dseeds);
   if (err != hipSuccess)
@@ -711,6 +715,7 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   a.d = e->d; a.R = R; a.gibbs = e->has_gibbs ? 1 : 0;
   a.normal = (!e->has_gibbs && e->k.prop == PBH_PROP_GAUSS) ? 1 : 0;
   a.vardelta = (!e->has_gibbs && e->k.prop == PBH_PROP_VARDELTA) ? 1 : 0;
+  a.db = e->mt_db ? 1 : 0;
   a.vmode = e->k.vmode;
   a.vdelta = e->k.pdel;
   hipError_t err = pbh::launch_legacy_gen(a, e->stream);

@@ -151,13 +151,14 @@ struct LegacyArgs {
   double *out;          // replay rows [n_steps][R][n]
   int64_t n, n_steps, step0;
   int32_t d, R, gibbs, normal;
+  int32_t db;           // double-buffered state [2][624][n] (legacy_gen_db)
   int32_t vardelta;     // VARDELTA: per-dim modes vmode, steps vdelta [d]
   uint64_t vmode;
   const double *vdelta;
 };
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
-                              int64_t n, hipStream_t s);
+                              int64_t n, int32_t db, hipStream_t s);
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s);
 
 // bool_perm_freq histogram (pbh_likelihoods.hip); counts must be zeroed,

@@ -46,6 +46,7 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *po
 }
 
 struct Mt {
+  static constexpr bool kLockstep = false;
   uint32_t *key;
   int64_t n, c;
   int pos;
@@ -107,8 +108,97 @@ struct Mt {
   }
 };
 
+// The same generator with a DOUBLE-BUFFERED state [2][624][N] and a
+// wave-synchronous refill.  A lane consumes block b from buffer `buf`; the
+// other buffer already holds block b + 1, so reaching word 624 only flips
+// `buf` and marks the lane pending (the buffer it left is free).  A pending
+// lane's free buffer is refilled with block b + 2 by an OUT-OF-PLACE twist of
+// its current block -- the sequential twist's result: dst[i] = src[i + 397]
+// (i < 227) or dst[i - 227] (i >= 227) ^ f(src[i], src[i + 1]), dst[623] =
+// dst[396] ^ f(src[623], dst[0]) -- and every pending lane of the wave twists
+// together, as soon as any of them is kRefill words into its block.  Lanes
+// drift apart by a few dozen words per block (polar rejections), so a wave
+// twists about once per 624 words instead of once per distinct lane position,
+// and every twist load / store is coalesced over the wave's pending lanes.
+// A lane always passes kRefill < 624 before its block ends, so the next
+// block is ready whenever it is needed, whatever the drift.
+// Per-lane state word: pos | buf << 16 | pending << 17.
+struct Mt2 {
+  static constexpr bool kLockstep = true;
+  uint32_t *key;
+  int64_t n, c;
+  int pos, buf, pend;
+  static constexpr int kRefill = 312;
+  static constexpr int kB = 16;
+
+  __device__ __forceinline__ uint32_t &k(int b, int i) {
+    return key[((int64_t)b * kN + i) * n + c];
+  }
+
+  __device__ __forceinline__ void twist_chunk(int s, int i0, int cnt) {
+    const int d = s ^ 1;
+    uint32_t nx[kB + 1], src[kB];
+#pragma unroll
+    for (int u = 0; u <= kB; ++u)
+      if (u <= cnt) nx[u] = k(s, i0 + u);
+#pragma unroll
+    for (int u = 0; u < kB; ++u)
+      if (u < cnt) {
+        const int i = i0 + u;
+        src[u] = i < kN - kM ? k(s, i + kM) : k(d, i + kM - kN);
+      }
+#pragma unroll
+    for (int u = 0; u < kB; ++u)
+      if (u < cnt) {
+        const uint32_t y = (nx[u] & kUpper) | (nx[u + 1] & kLower);
+        k(d, i0 + u) = src[u] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+      }
+  }
+
+  // block in buffer s -> next block in buffer s ^ 1
+  __device__ void twist_from(int s) {
+    const int d = s ^ 1;
+    for (int i = 0; i < kN - kM; i += kB)          // [0, 227): old words
+      twist_chunk(s, i, (kN - kM) - i < kB ? (kN - kM) - i : kB);
+    for (int i = kN - kM; i < kN - 1; i += kB)     // [227, 623): new words
+      twist_chunk(s, i, (kN - 1) - i < kB ? (kN - 1) - i : kB);
+    const uint32_t y = (k(s, kN - 1) & kUpper) | (k(d, 0) & kLower);
+    k(d, kN - 1) = k(d, kM - 1) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+  }
+
+  __device__ __forceinline__ uint32_t next32() {
+    if (__builtin_amdgcn_ballot_w64(pend && pos >= kRefill)) {   // wave-uniform
+      if (pend) {
+        twist_from(buf);
+        pend = 0;
+      }
+    }
+    if (pos == kN) {
+      buf ^= 1;
+      pos = 0;
+      pend = 1;
+    }
+    uint32_t y = k(buf, pos++);
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  __device__ __forceinline__ double next_double() {
+    const int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+
+  __device__ __forceinline__ int packed() const {
+    return pos | (buf << 16) | (pend << 17);
+  }
+};
+
 // legacy_gauss: polar method, second deviate cached across calls
-__device__ __forceinline__ double legacy_gauss(Mt &m, double &gauss, int &has) {
+template <class M>
+__device__ __forceinline__ double legacy_gauss(M &m, double &gauss, int &has) {
   if (has) {
     const double t = gauss;
     has = 0;
@@ -131,7 +221,8 @@ __device__ __forceinline__ double legacy_gauss(Mt &m, double &gauss, int &has) {
 // use_masked=True): bounds truncated toward zero, rng = hi - 1 - lo, then
 // words & mask (the smallest all-ones >= rng) until <= rng
 // (distributions.c buffered_bounded_masked_uint32).
-__device__ __forceinline__ double legacy_randint(Mt &m, double d0) {
+template <class M>
+__device__ __forceinline__ double legacy_randint(M &m, double d0) {
   const int64_t lo = (int64_t)trunc(-d0), hi = (int64_t)trunc(d0);
   const uint32_t rng = (uint32_t)(hi - 1 - lo);
   if (rng == 0) return (double)lo;
@@ -144,10 +235,31 @@ __device__ __forceinline__ double legacy_randint(Mt &m, double d0) {
   return (double)(lo + (int64_t)v);
 }
 
-__global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
+// Seeding for the double-buffered state: init_genrand into buffer 0, then
+// the first twist (which the reference makes at its first draw) into buffer 1:
+// the lane starts at word 0 of buffer 1 with buffer 0 free (pending).
+__global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t *pos,
+                                                         double *gauss, int32_t *has_gauss,
+                                                         const uint32_t *seeds, int64_t n) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.n) return;
-  Mt m{a.key, a.n, c, a.pos[c]};
+  if (c >= n) return;
+  uint32_t s = seeds[c];
+  for (int i = 0; i < kN; ++i) {
+    key[(int64_t)i * n + c] = s;
+    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(i + 1);
+  }
+  Mt2 m{key, n, c, 0, 0, 0};
+  m.twist_from(0);
+  m.buf = 1;
+  m.pos = 0;
+  m.pend = 1;
+  pos[c] = m.packed();
+  gauss[c] = 0.0;
+  has_gauss[c] = 0;
+}
+
+template <class M>
+__device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m) {
   double gauss = a.gauss[c];
   int has = a.has_gauss[c];
   const int64_t rowlen = (int64_t)a.R * a.n;
@@ -176,31 +288,91 @@ __global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
       row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
       continue;
     }
+    if (M::kLockstep && a.normal) {
+      // the step's d polar-method normals, lanes in lockstep over ATTEMPTS:
+      // each lane makes one attempt per iteration until it holds its pairs,
+      // so a wave loops ~max over lanes of the step's attempts (about 9.5
+      // for 5 pairs) instead of the sum over pairs of the per-pair maxima
+      // (about 18).  The draws, their order and the cached deviate are
+      // legacy_gauss's exactly.
+      int j = 0;
+      if (has) {
+        row[(int64_t)a.order[0] * a.n] = gauss;
+        has = 0;
+        gauss = 0.0;
+        j = 1;
+      }
+      while (__builtin_amdgcn_ballot_w64(j < a.d)) {   // wave-uniform
+        if (j < a.d) {
+          const double x1 = 2.0 * m.next_double() - 1.0;
+          const double x2 = 2.0 * m.next_double() - 1.0;
+          const double r2 = x1 * x1 + x2 * x2;
+          if (r2 < 1.0 && r2 != 0.0) {
+            const double f = sqrt(-2.0 * log(r2) / r2);
+            row[(int64_t)a.order[j] * a.n] = f * x2;
+            if (++j < a.d) {
+              row[(int64_t)a.order[j] * a.n] = f * x1;
+              ++j;
+            } else {
+              gauss = f * x1;   // cached for the next draw (odd d)
+              has = 1;
+            }
+          }
+        }
+      }
+      row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
+      continue;
+    }
     for (int j = 0; j < a.d; ++j) {
       const double v = a.normal ? legacy_gauss(m, gauss, has) : m.next_double();
       row[(int64_t)a.order[j] * a.n] = v;    // draw j feeds dim order[j]
     }
     row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
   }
-  a.pos[c] = m.pos;
   a.gauss[c] = gauss;
   a.has_gauss[c] = has;
+}
+
+__global__ __launch_bounds__(256) void legacy_gen_kernel(LegacyArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  Mt m{a.key, a.n, c, a.pos[c]};
+  legacy_gen_body(a, c, m);
+  a.pos[c] = m.pos;
+}
+
+// Lanes past the last chain leave at once; the refill ballot counts the
+// active lanes only.
+__global__ __launch_bounds__(256) void legacy_gen_db_kernel(LegacyArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  const int st = a.pos[c];
+  Mt2 m{a.key, a.n, c, st & 0xFFFF, (st >> 16) & 1, (st >> 17) & 1};
+  legacy_gen_body(a, c, m);
+  a.pos[c] = m.packed();
 }
 
 }  // namespace
 
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
-                              int64_t n, hipStream_t s) {
+                              int64_t n, int32_t db, hipStream_t s) {
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  hipLaunchKernelGGL(mt_seed_kernel, grid, block, 0, s, key, pos, gauss,
-                     has_gauss, seeds, n);
+  if (db)
+    hipLaunchKernelGGL(mt_seed_db_kernel, grid, block, 0, s, key, pos, gauss,
+                       has_gauss, seeds, n);
+  else
+    hipLaunchKernelGGL(mt_seed_kernel, grid, block, 0, s, key, pos, gauss,
+                       has_gauss, seeds, n);
   return hipGetLastError();
 }
 
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
   const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
-  hipLaunchKernelGGL(legacy_gen_kernel, grid, block, 0, s, a);
+  if (a.db)
+    hipLaunchKernelGGL(legacy_gen_db_kernel, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(legacy_gen_kernel, grid, block, 0, s, a);
   return hipGetLastError();
 }
 
