@@ -737,4 +737,49 @@ class Sampler:
     s = sel(self.tr['s']) if 's' in self.tr else None
     t = None if self.thresholds is None else sel(self.thresholds)
     v = pd('v_x', 'v_p')
-    return OPQRSTUV(None, pd('p_x', 'p_p'), None, None, s, t, u, v)
+    o, q, r = self._oqr(idx, sel)
+    return OPQRSTUV(o, pd('p_x', 'p_p'), q, r, s, t, u, v)
+
+  def _oqr(self, idx, sel):
+    """The summary's o, q and r (sp.py:160-191, sd.py:253-288): o = the
+    predecessor (the last accepted state; None on step 1, so summated over
+    the steps after the first), q = the transition PD over (x', x) with the
+    tran's value as prob, r = the reverse PD over (x, x') for an asymmetric
+    tran, whose value equals q's (rf.py:536, App. A-6).  q and r need the
+    recorded proposals (debug traces; single-chain samplers record them) and
+    are None for Gibbs."""
+    tr, names = self.tr, self.names
+    if self.spec.get('kind') == 'linreg' or self.spec['scores'] == 'gibbs':
+      return None, None, None
+    vx, vp = tr['v_x'], tr['v_p']                 # [N, T, d], [N, T]
+    later = idx[idx > 0]
+    o = None
+    if later.size:
+      sel_o = (lambda a: a[0, later - 1]) if not self.batched else \
+          (lambda a: np.moveaxis(a[:, later - 1], 0, 1))
+      o = PD('p', {k: sel_o(vx[..., i]) for i, k in enumerate(names)},
+             prob=sel_o(vp), pscale=self.pscale)
+    if 'p_x' not in tr:
+      return o, None, None
+    init = self._init_array()                      # [N, d]
+    prev = np.concatenate([init[:, None, :], vx[:, :-1, :]], axis=1)
+    px = tr['p_x']
+    tran = self.spec['tran']
+    if self.spec['scores'] == 'metropolis' and self.sp._tran_spec() is None:
+      qv = None
+    elif tran['kind'] == 'const':
+      qv = np.full(vp.shape, float(tran['value']))
+    else:   # prod over the tran's order of norm.pdf(x', x + offset, scale)
+      qv = None
+      for k in tran['order']:
+        term = scipy.stats.norm.pdf(px[..., k], loc=prev[..., k] + tran['offset'][k],
+                                    scale=tran['scale'])
+        qv = term if qv is None else qv * term
+    succ = {k + "'": sel(px[..., i]) for i, k in enumerate(names)}
+    pred = {k: sel(prev[..., i]) for i, k in enumerate(names)}
+    qprob = None if qv is None else sel(qv)
+    q = PD('q', dict(succ, **pred), prob=qprob, pscale=self.pscale)
+    r = None
+    if not tran.get('sym', True):
+      r = PD('r', dict(pred, **succ), prob=qprob, pscale=self.pscale)
+    return o, q, r

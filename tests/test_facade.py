@@ -297,3 +297,37 @@ def test_mixture_densities_trace_or_fail_loudly():
     process.set_prob(fn, pscale='log')
     with pytest.raises(pb.NotLowerable):
       process.lower()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['mcmc_prob6', 'diag10', 'metrohast_norm1d',
+                                  'mcmc_prob2'])
+def test_summary_o_q_r_match_reference(name):
+  """SP(samples).o / .q / .r (sp.py:160-191) against the reference's own
+  summary of the same seeded chain (tools/gen_summary_golden.py): o is the
+  last accepted state from step 2 on, q the transition PD over (x', x) with
+  the tran's value, r (asymmetric trans) its reverse with the same value.
+  The reference's o / p also carry the iid data key as a set of sizes; the
+  variable keys are compared."""
+  import json
+  import os
+  g = np.load(os.path.join(os.path.dirname(__file__), 'golden',
+                           'summary_oqr.npz'))
+  meta = json.loads(str(g['meta']))[name]
+  builder, params, n, t, seed0 = WORKLOADS[name]
+  process, init, extra, kwds, keys, _ = _build(name)
+  np.random.seed(meta['seed'])
+  args = (init,) if extra is None else (init, extra)
+  summary = process(process.walk(process.sampler(*args, stop=meta['steps'],
+                                                 **kwds)))
+  for f, fkeys in meta['fields'].items():
+    d = getattr(summary, f)
+    if fkeys is None:
+      assert d is None, f
+      continue
+    assert list(d.keys()) == fkeys, (f, list(d.keys()))
+    for k in fkeys:
+      ref = g['{}/{}/{}'.format(name, f, k)]
+      assert _golden_rtol(np.ravel(d[k]), ref) <= 1e-12, (f, k)
+    ref = g['{}/{}/prob'.format(name, f)]
+    assert _golden_rtol(np.ravel(d.prob), ref) <= 1e-12, (f, 'prob')
