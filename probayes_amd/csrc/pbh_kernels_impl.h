@@ -161,11 +161,15 @@ __device__ __forceinline__ double gmm_fast(const KArgs &a, const double (&x)[D])
   return m + log(sum);
 }
 
+// lx (production, may be null): log of x for the dims with the (log, exp)
+// ufun, as the proposal formed them (x' = exp(log x + delta)), so the
+// density need not take the log of x' again.
 template <int D, int TGT, bool FAST>
 __device__ __forceinline__ double joint_density(const KArgs &a,
                                                 const double (&x)[D],
                                                 const double *obs_lds,
-                                                bool use_lds) {
+                                                bool use_lds,
+                                                const double *lx = nullptr) {
   double out = 0.0;
   switch (TGT ? TGT : a.target) {
     case PBH_TARGET_DIAG_GAUSS: {
@@ -192,14 +196,29 @@ __device__ __forceinline__ double joint_density(const KArgs &a,
         if (k == a.i0) mu = x[k];
         if (k == a.i1) sg = x[k];
       }
-      const double lsg = FAST ? fast_log(sg) : log(sg);
+      double lsg = 0.;
+      if (!FAST) {
+        lsg = log(sg);
+      } else {
+        double l = 0.;
+        bool have = false;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          if (k == a.i1 && lx && ((a.ufun >> k) & 1u)) { l = lx[k]; have = true; }
+        lsg = have ? l : fast_log(sg);
+      }
       const double logC = a.norm_logC;
       if (FAST) {
-        // production path: sufficient statistics (obar, S2) of the data
+        // production path: sufficient statistics (obar, S2) of the data;
+        // 1 / sigma^2 by the hardware reciprocal + two Newton steps
         const double n = (double)a.tn;
         const double dm = cld(a.tw, 0) - mu;
         const double ss = __builtin_fma(n * dm, dm, cld(a.tw, 1));
-        out = -0.5 * ss / (sg * sg) - n * (logC + lsg);
+        const double s2 = sg * sg;
+        double ri = __builtin_amdgcn_rcp(s2);
+        ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+        ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+        out = -0.5 * ss * ri - n * (logC + lsg);
       } else if (use_lds) {
         out = np_pairwise(
             [&](int64_t j) { return norm_logpdf(obs_lds[j], mu, sg, lsg, logC); },
@@ -507,7 +526,9 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       thr = u01(w.x, w.y);
     }
     // ---- proposal ----
-    double xp[D];
+    double xp[D], lxp[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) lxp[k] = 0.;
     {
       double dl[D];
       if (prop == PBH_PROP_GAUSS) {
@@ -547,27 +568,47 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         }
         const double ss = np_sum_regs<D>(sq, D);
         const double rss = ss >= kNearlyPosZero ? sqrt(ss) : 0.;
+        if (FAST) {
+          // production: one division for the radius scale
+          const double sc = d0 / rss;
 #pragma unroll
-        for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * cld(a.plen, k);
+          for (int k = 0; k < D; ++k) dl[k] = (dl[k] * sc) * cld(a.plen, k);
+        } else {
+#pragma unroll
+          for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * cld(a.plen, k);
+        }
       }
       if (a.has_tfun) apply_tfun<D>(a.ptf, dl);   // wave-uniform
 #pragma unroll
-      for (int k = 0; k < D; ++k)
-        xp[k] = ((a.ufun >> k) & 1u)
-                    ? (FAST ? fast_exp(fast_log(x[k]) + dl[k]) : exp(log(x[k]) + dl[k]))
-                    : x[k] + dl[k];
+      for (int k = 0; k < D; ++k) {
+        if ((a.ufun >> k) & 1u) {
+          if (FAST) {
+            lxp[k] = fast_log(x[k]) + dl[k];
+            xp[k] = fast_exp(lxp[k]);
+          } else {
+            xp[k] = exp(log(x[k]) + dl[k]);
+          }
+        } else {
+          xp[k] = x[k] + dl[k];
+        }
+      }
       if (a.vint | a.bnd_on) {   // wave-uniform: int variables, bound=True
 #pragma unroll
         for (int k = 0; k < D; ++k) {
+          const double v0 = xp[k];
           if ((a.vint >> k) & 1u) xp[k] = trunc(xp[k]);
           if ((a.bnd_on >> k) & 1u)
             xp[k] = bound_value(xp[k], x[k], cld(a.blo, k), cld(a.bhi, k),
                                 (a.bnd_xlo >> k) & 1u, (a.bnd_xhi >> k) & 1u);
+          // a clamped / bounced ufun value: its log is taken afresh
+          if (FAST && ((a.ufun >> k) & 1u) && !(xp[k] == v0))
+            lxp[k] = fast_log(xp[k]);
         }
       }
     }
     // ---- density, score, accept ----
-    const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds);
+    const double lpp = joint_density<D, TGT, FAST>(a, xp, s_obs, use_lds,
+                                                   FAST ? lxp : nullptr);
     double eA = 0.;
     double sc = __builtin_nan("");
     bool acc;
