@@ -108,62 +108,101 @@ struct Mt {
   }
 };
 
-// The same generator with a DOUBLE-BUFFERED state [2][624][N] and a
-// wave-synchronous refill.  A lane consumes block b from buffer `buf`; the
-// other buffer already holds block b + 1, so reaching word 624 only flips
-// `buf` and marks the lane pending (the buffer it left is free).  A pending
-// lane's free buffer is refilled with block b + 2 by an OUT-OF-PLACE twist of
-// its current block -- the sequential twist's result: dst[i] = src[i + 397]
-// (i < 227) or dst[i - 227] (i >= 227) ^ f(src[i], src[i + 1]), dst[623] =
-// dst[396] ^ f(src[623], dst[0]) -- and every pending lane of the wave twists
-// together, as soon as any of them is kRefill words into its block.  Lanes
-// drift apart by a few dozen words per block (polar rejections), so a wave
-// twists about once per 624 words instead of once per distinct lane position,
-// and every twist load / store is coalesced over the wave's pending lanes.
-// A lane always passes kRefill < 624 before its block ends, so the next
-// block is ready whenever it is needed, whatever the drift.
+// The same generator with a DOUBLE-BUFFERED state and a wave-synchronous
+// refill.  A lane consumes block b from buffer `buf`; the other buffer
+// already holds block b + 1, so reaching word 624 only flips `buf` and marks
+// the lane pending (the buffer it left is free).  A pending lane's free
+// buffer is refilled with block b + 2 by an OUT-OF-PLACE twist of its current
+// block -- the sequential twist's result: dst[i] = src[i + 397] (i < 227) or
+// dst[i - 227] (i >= 227) ^ f(src[i], src[i + 1]), dst[623] = dst[396] ^
+// f(src[623], dst[0]) -- and every pending lane of the wave twists together,
+// as soon as any of them is kRefill words into its block.  Lanes drift apart
+// by a few dozen words per block (polar rejections), so a wave twists about
+// once per 624 words instead of once per distinct lane position.  A lane
+// always passes kRefill < 624 before its block ends, so the next block is
+// ready whenever it is needed, whatever the drift.
+//
+// Layout [2][156][N] of uint4: a lane's words 4q .. 4q + 3 are one 16-byte
+// quad, so the drifting lanes read their words 16 bytes at a time (a
+// register quad, reloaded every fourth word) and the twist moves whole
+// quads: each quad of dst needs the quad q of src and the first word of quad
+// q + 1, words 4q + 397 .. + 400 (quads q + 99, q + 100, at offset 1) or
+// dst words 4q - 227 .. - 224 (quads q - 57, q - 56, at offset 1).
 // Per-lane state word: pos | buf << 16 | pending << 17.
+constexpr int kQ = kN / 4;   // 156 quads per block
+
+__device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b) {
+  const uint32_t y = (a & kUpper) | (b & kLower);
+  return (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+}
+
 struct Mt2 {
   static constexpr bool kLockstep = true;
-  uint32_t *key;
+  static constexpr int kRefill = 312;
+  uint4 *key;
   int64_t n, c;
   int pos, buf, pend;
-  static constexpr int kRefill = 312;
-  static constexpr int kB = 16;
+  uint4 cur;   // the quad holding word pos (valid when pos % 4 != 0)
 
-  __device__ __forceinline__ uint32_t &k(int b, int i) {
-    return key[((int64_t)b * kN + i) * n + c];
-  }
-
-  __device__ __forceinline__ void twist_chunk(int s, int i0, int cnt) {
-    const int d = s ^ 1;
-    uint32_t nx[kB + 1], src[kB];
-#pragma unroll
-    for (int u = 0; u <= kB; ++u)
-      if (u <= cnt) nx[u] = k(s, i0 + u);
-#pragma unroll
-    for (int u = 0; u < kB; ++u)
-      if (u < cnt) {
-        const int i = i0 + u;
-        src[u] = i < kN - kM ? k(s, i + kM) : k(d, i + kM - kN);
-      }
-#pragma unroll
-    for (int u = 0; u < kB; ++u)
-      if (u < cnt) {
-        const uint32_t y = (nx[u] & kUpper) | (nx[u + 1] & kLower);
-        k(d, i0 + u) = src[u] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-      }
+  __device__ __forceinline__ uint4 &q(int b, int i) {
+    return key[((int64_t)b * kQ + i) * n + c];
   }
 
   // block in buffer s -> next block in buffer s ^ 1
   __device__ void twist_from(int s) {
     const int d = s ^ 1;
-    for (int i = 0; i < kN - kM; i += kB)          // [0, 227): old words
-      twist_chunk(s, i, (kN - kM) - i < kB ? (kN - kM) - i : kB);
-    for (int i = kN - kM; i < kN - 1; i += kB)     // [227, 623): new words
-      twist_chunk(s, i, (kN - 1) - i < kB ? (kN - 1) - i : kB);
-    const uint32_t y = (k(s, kN - 1) & kUpper) | (k(d, 0) & kLower);
-    k(d, kN - 1) = k(d, kM - 1) ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+    uint4 a = q(s, 0);          // src quad i
+    uint4 hi0 = q(s, 99), hi1 = q(s, 100);   // src quads i + 99, i + 100
+    for (int i = 0; i < 56; ++i) {            // words 0 .. 223: src[w + 397]
+      const uint4 nx = q(s, i + 1);
+      uint4 o;
+      o.x = hi0.y ^ mt_f(a.x, a.y);
+      o.y = hi0.z ^ mt_f(a.y, a.z);
+      o.z = hi0.w ^ mt_f(a.z, a.w);
+      o.w = hi1.x ^ mt_f(a.w, nx.x);
+      q(d, i) = o;
+      a = nx;
+      hi0 = hi1;
+      if (i + 101 < kQ) hi1 = q(s, i + 101);   // (quad 156 is past the block)
+    }
+    {                                          // quad 56: words 224 .. 227
+      const uint4 nx = q(s, 57);
+      const uint4 d0 = q(d, 0);
+      uint4 o;
+      o.x = hi0.y ^ mt_f(a.x, a.y);            // src[621]
+      o.y = hi0.z ^ mt_f(a.y, a.z);            // src[622]
+      o.z = hi0.w ^ mt_f(a.z, a.w);            // src[623]
+      o.w = d0.x ^ mt_f(a.w, nx.x);            // dst[0]
+      q(d, 56) = o;
+      a = nx;
+    }
+    uint4 lo0 = q(d, 0), lo1 = q(d, 1);       // dst quads i - 57, i - 56
+    for (int i = 57; i < kQ - 1; ++i) {       // words 228 .. 619
+      const uint4 nx = q(s, i + 1);
+      uint4 o;
+      o.x = lo0.y ^ mt_f(a.x, a.y);
+      o.y = lo0.z ^ mt_f(a.y, a.z);
+      o.z = lo0.w ^ mt_f(a.z, a.w);
+      o.w = lo1.x ^ mt_f(a.w, nx.x);
+      q(d, i) = o;
+      a = nx;
+      lo0 = lo1;
+      lo1 = q(d, i - 55);
+    }
+    {                                          // quad 155: words 620 .. 623
+      const uint4 d0 = q(d, 0);
+      const uint4 d99 = q(d, 99);
+      uint4 o;
+      o.x = lo0.y ^ mt_f(a.x, a.y);            // dst[393]
+      o.y = lo0.z ^ mt_f(a.y, a.z);            // dst[394]
+      o.z = lo0.w ^ mt_f(a.z, a.w);            // dst[395]
+      o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
+      q(d, kQ - 1) = o;
+    }
+  }
+
+  __device__ __forceinline__ void load_cur() {
+    if (pos & 3) cur = q(buf, pos >> 2);
   }
 
   __device__ __forceinline__ uint32_t next32() {
@@ -178,7 +217,10 @@ struct Mt2 {
       pos = 0;
       pend = 1;
     }
-    uint32_t y = k(buf, pos++);
+    const int u = pos & 3;
+    if (u == 0) cur = q(buf, pos >> 2);
+    ++pos;
+    uint32_t y = u == 0 ? cur.x : (u == 1 ? cur.y : (u == 2 ? cur.z : cur.w));
     y ^= y >> 11;
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
@@ -243,12 +285,18 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
                                                          const uint32_t *seeds, int64_t n) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
+  uint4 *qk = reinterpret_cast<uint4 *>(key);
   uint32_t s = seeds[c];
-  for (int i = 0; i < kN; ++i) {
-    key[(int64_t)i * n + c] = s;
-    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(i + 1);
+  for (int i = 0; i < kQ; ++i) {
+    uint32_t w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      w[u] = s;
+      s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(4 * i + u + 1);
+    }
+    qk[(int64_t)i * n + c] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  Mt2 m{key, n, c, 0, 0, 0};
+  Mt2 m{qk, n, c, 0, 0, 0, make_uint4(0u, 0u, 0u, 0u)};
   m.twist_from(0);
   m.buf = 1;
   m.pos = 0;
@@ -259,7 +307,8 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
 }
 
 template <class M>
-__device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m) {
+__device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m,
+                                                double2 *stage = nullptr) {
   double gauss = a.gauss[c];
   int has = a.has_gauss[c];
   const int64_t rowlen = (int64_t)a.R * a.n;
@@ -289,34 +338,48 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       continue;
     }
     if (M::kLockstep && a.normal) {
-      // the step's d polar-method normals, lanes in lockstep over ATTEMPTS:
-      // each lane makes one attempt per iteration until it holds its pairs,
-      // so a wave loops ~max over lanes of the step's attempts (about 9.5
-      // for 5 pairs) instead of the sum over pairs of the per-pair maxima
-      // (about 18).  The draws, their order and the cached deviate are
+      // the step's d polar-method normals.  Lanes run the ATTEMPTS in
+      // lockstep (one per iteration until each holds its pairs: a wave loops
+      // ~max over lanes of the step's attempts, about 9.5 for 5 pairs, not
+      // the sum over pairs of per-pair maxima, about 18), keeping only the
+      // accepted (x1, x2) in LDS; the transcendental part f = sqrt(-2 ln r2 /
+      // r2) then runs over the step's pairs as independent chains.  The
+      // draws, their order, the arithmetic and the cached deviate are
       // legacy_gauss's exactly.
-      int j = 0;
+      int j0 = 0;
       if (has) {
         row[(int64_t)a.order[0] * a.n] = gauss;
         has = 0;
         gauss = 0.0;
-        j = 1;
+        j0 = 1;
       }
-      while (__builtin_amdgcn_ballot_w64(j < a.d)) {   // wave-uniform
-        if (j < a.d) {
+      const int need = (a.d - j0 + 1) / 2;   // pairs this lane draws
+      int np = 0;
+      while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+        if (np < need) {
           const double x1 = 2.0 * m.next_double() - 1.0;
           const double x2 = 2.0 * m.next_double() - 1.0;
           const double r2 = x1 * x1 + x2 * x2;
           if (r2 < 1.0 && r2 != 0.0) {
-            const double f = sqrt(-2.0 * log(r2) / r2);
-            row[(int64_t)a.order[j] * a.n] = f * x2;
-            if (++j < a.d) {
-              row[(int64_t)a.order[j] * a.n] = f * x1;
-              ++j;
-            } else {
-              gauss = f * x1;   // cached for the next draw (odd d)
-              has = 1;
-            }
+            stage[np * blockDim.x + threadIdx.x] = make_double2(x1, x2);
+            ++np;
+          }
+        }
+      }
+      const int kmax = (a.d + 1) / 2;
+#pragma unroll 4
+      for (int k = 0; k < kmax; ++k) {
+        if (k < need) {
+          const double2 p = stage[k * blockDim.x + threadIdx.x];
+          const double r2 = p.x * p.x + p.y * p.y;
+          const double f = sqrt(-2.0 * log(r2) / r2);
+          const int j = j0 + 2 * k;
+          row[(int64_t)a.order[j] * a.n] = f * p.y;
+          if (j + 1 < a.d) {
+            row[(int64_t)a.order[j + 1] * a.n] = f * p.x;
+          } else {
+            gauss = f * p.x;   // cached for the next draw (odd d)
+            has = 1;
           }
         }
       }
@@ -347,8 +410,12 @@ __global__ __launch_bounds__(256) void legacy_gen_db_kernel(LegacyArgs a) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.n) return;
   const int st = a.pos[c];
-  Mt2 m{a.key, a.n, c, st & 0xFFFF, (st >> 16) & 1, (st >> 17) & 1};
-  legacy_gen_body(a, c, m);
+  Mt2 m{reinterpret_cast<uint4 *>(a.key), a.n, c, st & 0xFFFF, (st >> 16) & 1,
+        (st >> 17) & 1, make_uint4(0u, 0u, 0u, 0u)};
+  m.load_cur();
+  // accepted polar pairs of one step, [pair][thread] (bank-conflict free)
+  __shared__ double2 s_stage[(PBH_MAX_DIM + 1) / 2 * 256];
+  legacy_gen_body(a, c, m, s_stage);
   a.pos[c] = m.packed();
 }
 
