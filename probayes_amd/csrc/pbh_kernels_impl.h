@@ -452,39 +452,13 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   // record (g + 1) / thin - 1 - rec_base.
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
-  // Production uniform draws (tuple / list / per-variable deltas) are
-  // software-pipelined: the raw Philox blocks of step g + 1 are computed in
-  // step g's body, where they are independent of its fp64 chain (the one-lane
-  // kernel runs one wavefront per SIMD at d = 2, so the scheduler needs that
-  // independent work to hide latency).  Same blocks, same draws.
-  constexpr bool PIPE = RNG == PBH_RNG_PHILOX && !TAB;
-  constexpr int PB = PIPE ? (D + 1) / 2 : 1;
-  u32x4 nblk[PB], nthr;
-  if constexpr (PIPE) {
-#pragma unroll
-    for (int p = 0; p < PB; ++p)
-      nblk[p] = philox4x32_10(ctr(p, a.g0, chain), a.seed_lo, a.seed_hi);
-    nthr = philox4x32_10(ctr(0xFFFFu, a.g0, chain), a.seed_lo, a.seed_hi);
-  }
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     // ---- draws ----
     double r[D];
     double thr;
     uint32_t tw0 = 0, tw1 = 0;   // threshold words: thr = u01(tw0, tw1)
-    if constexpr (PIPE) {
-#pragma unroll
-      for (int p = 0; p < PB; ++p) {
-        const u32x4 w = nblk[p];
-        r[2 * p] = u01(w.x, w.y);
-        if (2 * p + 1 < D) r[2 * p + 1] = u01(w.z, w.w);
-        nblk[p] = philox4x32_10(ctr(p, g + 1, chain), a.seed_lo, a.seed_hi);
-      }
-      tw0 = nthr.x;
-      tw1 = nthr.y;
-      thr = u01(tw0, tw1);
-      nthr = philox4x32_10(ctr(0xFFFFu, g + 1, chain), a.seed_lo, a.seed_hi);
-    } else if (RNG == PBH_RNG_REPLAY) {
+    if (RNG == PBH_RNG_REPLAY) {
       const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
 #pragma unroll
       for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
