@@ -456,8 +456,12 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     const int64_t g = a.g0 + s;
     // ---- draws ----
     double r[D];
-    double thr;
+    double thr = 0.;
     uint32_t tw0 = 0, tw1 = 0;   // threshold words: thr = u01(tw0, tw1)
+    // production Philox: t's leading lead_bits bits are `lead`, the rest come
+    // from block lead_ctr (drawn on demand when the filter decides alone)
+    uint32_t lead = 0, lead_ctr = 0;
+    int lead_bits = 0;
     if (RNG == PBH_RNG_REPLAY) {
       const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
 #pragma unroll
@@ -488,8 +492,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     } else if (TAB && prop == PBH_PROP_GAUSS) {
       // one bm64 fp64 normal pair per Philox block; t's leading 14 bits are
       // block 0's spare bits, the rest come from block 0x40 -- the same t
-      // as the multi-lane GMM kernel's (its lead + fallback block)
-      uint32_t lead = 0;
+      // as the multi-lane GMM kernel's (its lead + fallback block).  The
+      // filter needs only the lead: block 0x40 is drawn when it cannot decide.
 #pragma unroll
       for (int p = 0; p < (D + 1) / 2; ++p) {
         const u32x4 w = philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi);
@@ -499,10 +503,36 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         if (2 * p + 1 < D) r[2 * p + 1] = z1;
         if (p == 0) lead = bm64_spare(w.x, w.z);
       }
-      const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
-      tw0 = (lead << 18) | (w.x >> 14);
-      tw1 = w.y;
-      thr = u01(tw0, tw1);
+      lead_bits = 14;
+      lead_ctr = 0x40u;
+      if (!simple) {
+        const u32x4 w = philox4x32_10(ctr(lead_ctr, g, chain), a.seed_lo, a.seed_hi);
+        tw0 = (lead << 18) | (w.x >> 14);
+        tw1 = w.y;
+        thr = u01(tw0, tw1);
+      }
+    } else if (RNG == PBH_RNG_PHILOX && prop != PBH_PROP_GAUSS) {
+      // production uniform draws: t's leading 22 bits are the spare low bits
+      // of block 0's words (u01 keeps the top 27 + 26 bits of each pair; at
+      // d = 1 the unused word z gives them), the rest come from block 0xFFFF,
+      // drawn when the filter cannot decide (or every step without it)
+#pragma unroll
+      for (int p = 0; p < (D + 1) / 2; ++p) {
+        const u32x4 w = philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi);
+        r[2 * p] = u01(w.x, w.y);
+        if (2 * p + 1 < D) r[2 * p + 1] = u01(w.z, w.w);
+        if (p == 0)
+          lead = ((w.x & 31u) << 17) | ((w.y & 63u) << 11) |
+                 (D >= 2 ? (((w.z & 31u) << 6) | (w.w & 63u)) : (w.z >> 21));
+      }
+      lead_bits = 22;
+      lead_ctr = 0xFFFFu;
+      if (!simple) {
+        const u32x4 w = philox4x32_10(ctr(lead_ctr, g, chain), a.seed_lo, a.seed_hi);
+        tw0 = (lead << 10) | (w.x >> 22);
+        tw1 = w.y;
+        thr = u01(tw0, tw1);
+      }
     } else {
       if (prop == PBH_PROP_GAUSS) {
 #pragma unroll
@@ -620,10 +650,19 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       // the ratio form's decision through the filter (see mh_pair_kernel);
       // a constant tuple tran scales both log-probs by q~ (App. A-1)
       const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
-      const Decision dc = accept_filter(bA, bB, tw0, lin);
+      const Decision dc = lead_bits == 14 ? accept_filter_lead<14>(bA, bB, lead, lin)
+                        : lead_bits == 22 ? accept_filter_lead<22>(bA, bB, lead, lin)
+                                          : accept_filter(bA, bB, tw0, lin);
       acc = dc.acc;
       if (__ballot(dc.need)) {   // wave-uniform, rare
-        if (dc.need) acc = ratio_accept(bA, bB, u01(tw0, tw1), lin, a.log_npi);
+        if (dc.need) {
+          if (lead_bits) {   // t's remaining bits
+            const u32x4 w = philox4x32_10(ctr(lead_ctr, g, chain), a.seed_lo, a.seed_hi);
+            tw0 = (lead << (32 - lead_bits)) | (w.x >> lead_bits);
+            tw1 = w.y;
+          }
+          acc = ratio_accept(bA, bB, u01(tw0, tw1), lin, a.log_npi);
+        }
       }
     } else {
       eA = lin ? lpp : (FAST ? exp_logp_fast(lpp, a.log_npi)
