@@ -47,6 +47,7 @@ struct pbh_engine {
   uint32_t *mt_key = nullptr;
   bool mt_db = false;          // mt_key is [2][624][n] (double-buffered)
   bool legacy_db = true;       // PBH_LEGACY_DB=0: the in-place state
+  bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
   // trace
@@ -198,6 +199,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
+  if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreate(&e->ev0);
   if (err == hipSuccess) err = hipEventCreate(&e->ev1);
@@ -716,6 +718,7 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   a.normal = (!e->has_gibbs && e->k.prop == PBH_PROP_GAUSS) ? 1 : 0;
   a.vardelta = (!e->has_gibbs && e->k.prop == PBH_PROP_VARDELTA) ? 1 : 0;
   a.db = e->mt_db ? 1 : 0;
+  a.win = e->legacy_win ? 1 : 0;
   a.vmode = e->k.vmode;
   a.vdelta = e->k.pdel;
   hipError_t err = pbh::launch_legacy_gen(a, e->stream);

@@ -152,6 +152,7 @@ struct LegacyArgs {
   int64_t n, n_steps, step0;
   int32_t d, R, gibbs, normal;
   int32_t db;           // double-buffered state [2][624][n] (legacy_gen_db)
+  int32_t win;          // with db: consume through the LDS window (Mt3)
   int32_t vardelta;     // VARDELTA: per-dim modes vmode, steps vdelta [d]
   uint64_t vmode;
   const double *vdelta;

@@ -27,6 +27,7 @@ namespace pbh {
 namespace {
 
 constexpr int kN = 624, kM = 397;
+constexpr int kBlockLegacy = 256;   // threads per workgroup of the generators
 constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
 
 __global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *pos,
@@ -106,6 +107,7 @@ struct Mt {
     const int32_t a = (int32_t)(next32() >> 5), b = (int32_t)(next32() >> 6);
     return (a * 67108864.0 + b) / 9007199254740992.0;
   }
+  __device__ __forceinline__ void maintain() {}
 };
 
 // The same generator with a DOUBLE-BUFFERED state and a wave-synchronous
@@ -236,6 +238,221 @@ struct Mt2 {
   __device__ __forceinline__ int packed() const {
     return pos | (buf << 16) | (pend << 17);
   }
+  __device__ __forceinline__ void maintain() {}
+};
+
+// The double-buffered state consumed through an LDS WINDOW (the default).
+// Mt2's lanes read their next quad from HBM when they reach it: in the
+// polar-method loop that is one dependent global load per attempt, and at one
+// wavefront per SIMD nothing hides it.  Here each lane's upcoming words are
+// staged in LDS ahead of use: a ring of 2H quads per lane ([slot][256
+// threads] of uint4, conflict-free whatever the lanes' positions), refilled H
+// quads at a time (H loads in flight) at the top of a step whenever a lane
+// has H or fewer quads left -- the ballot makes the refills wave-wide.  The
+// head (next quad to load) runs at most 2H quads ahead of the consumption
+// position, so it is inside the current block or the next one; the next
+// block must be twisted before the head enters it (forced here if the step-top
+// trigger at word 312 has not yet run).  A twist overwrites only the block
+// BEFORE the consumption position's, whose words are consumed, so the state
+// in HBM (pos, buf, pend: Mt2's packed word) stays valid when a launch ends
+// with words still in the window.
+//
+// The twist itself runs in batches of 14 quads: part 1 (dst quads 0 .. 55)
+// reads src quads i .. i + 14 and i + 99 .. i + 113, part 2 (quads 57 ..
+// 154) src quads i .. i + 14 and dst quads i - 57 .. i - 43 (written by part
+// 1 or an earlier batch), so ~30 loads are in flight instead of two.
+// a quad as a plain vector (SROA splits arrays of it into registers; arrays
+// of HIP's uint4 struct stayed in scratch)
+typedef uint32_t w4 __attribute__((ext_vector_type(4)));
+
+template <int H>
+struct Mt3 {
+  static constexpr bool kLockstep = true;
+  static constexpr int kRefill = 312;
+  static constexpr int kW = 2 * H;   // window quads per lane (a power of two)
+  static constexpr int kTB = 14;     // twist batch (56 = 4 x 14, 98 = 7 x 14)
+  w4 *key;
+  int64_t n, c;
+  int pos, buf, pend;
+  int blk;      // launch-relative block of pos
+  int hq;       // launch-relative index of the next quad to load
+  w4 cur;
+  w4 *win;   // this lane's slot 0 (slot stride blockDim.x)
+
+  __device__ __forceinline__ w4 &q(int b, int i) {
+    return key[((int64_t)b * kQ + i) * n + c];
+  }
+  __device__ __forceinline__ w4 &slot(int k) {
+    return win[(k & (kW - 1)) * kBlockLegacy];
+  }
+  __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
+
+  __device__ __forceinline__ void twist_from(int s) {
+    const int d = s ^ 1;
+    for (int i0 = 0; i0 < 56; i0 += kTB) {
+      w4 a[kTB + 1], h[kTB + 1];
+#pragma unroll
+      for (int u = 0; u <= kTB; ++u) {
+        a[u] = q(s, i0 + u);
+        h[u] = q(s, i0 + 99 + u);
+      }
+#pragma unroll
+      for (int u = 0; u < kTB; ++u) {
+        w4 o;
+        o.x = h[u].y ^ mt_f(a[u].x, a[u].y);
+        o.y = h[u].z ^ mt_f(a[u].y, a[u].z);
+        o.z = h[u].w ^ mt_f(a[u].z, a[u].w);
+        o.w = h[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+        q(d, i0 + u) = o;
+      }
+    }
+    {                                          // quad 56: words 224 .. 227
+      const w4 a = q(s, 56), nx = q(s, 57), h = q(s, 155), d0 = q(d, 0);
+      w4 o;
+      o.x = h.y ^ mt_f(a.x, a.y);              // src[621]
+      o.y = h.z ^ mt_f(a.y, a.z);              // src[622]
+      o.z = h.w ^ mt_f(a.z, a.w);              // src[623]
+      o.w = d0.x ^ mt_f(a.w, nx.x);            // dst[0]
+      q(d, 56) = o;
+    }
+    for (int i0 = 57; i0 < kQ - 1; i0 += kTB) {
+      w4 a[kTB + 1], l[kTB + 1];
+#pragma unroll
+      for (int u = 0; u <= kTB; ++u) {
+        a[u] = q(s, i0 + u);
+        l[u] = q(d, i0 - 57 + u);
+      }
+#pragma unroll
+      for (int u = 0; u < kTB; ++u) {
+        w4 o;
+        o.x = l[u].y ^ mt_f(a[u].x, a[u].y);
+        o.y = l[u].z ^ mt_f(a[u].y, a[u].z);
+        o.z = l[u].w ^ mt_f(a[u].z, a[u].w);
+        o.w = l[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+        q(d, i0 + u) = o;
+      }
+    }
+    {                                          // quad 155: words 620 .. 623
+      const w4 a = q(s, kQ - 1), d0 = q(d, 0), d98 = q(d, 98), d99 = q(d, 99);
+      w4 o;
+      o.x = d98.y ^ mt_f(a.x, a.y);            // dst[393]
+      o.y = d98.z ^ mt_f(a.y, a.z);            // dst[394]
+      o.z = d98.w ^ mt_f(a.z, a.w);            // dst[395]
+      o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
+      q(d, kQ - 1) = o;
+    }
+  }
+
+  // quads hq .. hq + H - 1 into the ring (their slots' quads are consumed)
+  __device__ __forceinline__ void refill() {
+    const int nb = (blk + 1) * kQ;   // first quad of the next block
+    if (pend && hq + H > nb) {       // the head enters the next block
+      twist_from(buf);
+      pend = 0;
+    }
+    w4 v[H];
+#pragma unroll
+    for (int u = 0; u < H; ++u) {
+      const int k = hq + u;
+      const bool nx = k >= nb;
+      v[u] = q(buf ^ (nx ? 1 : 0), nx ? k - nb : k - blk * kQ);
+    }
+#pragma unroll
+    for (int u = 0; u < H; ++u) slot(hq + u) = v[u];
+    hq += H;
+  }
+
+  __device__ __forceinline__ void init(int st, w4 *w) {
+    pos = st & 0xFFFF;
+    buf = (st >> 16) & 1;
+    pend = (st >> 17) & 1;
+    blk = 0;
+    win = w;
+    if (pend && pos >= kRefill) {
+      twist_from(buf);
+      pend = 0;
+    }
+    hq = pos >> 2;
+    refill();
+    refill();
+    if (pos & 3) cur = slot(aq());
+  }
+
+  // wave-uniform point (top of a step): the refill twist, then the window
+  __device__ __forceinline__ void maintain() {
+    if (__builtin_amdgcn_ballot_w64(pend && pos >= kRefill)) {
+      if (pend) {   // every pending lane: its free buffer holds a consumed block
+        twist_from(buf);
+        pend = 0;
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(hq - aq() <= H)) {
+      if (hq - aq() <= H) refill();
+    }
+  }
+
+  __device__ __forceinline__ uint32_t next32() {
+    if (pos == kN) {
+      buf ^= 1;
+      pos = 0;
+      pend = 1;
+      ++blk;
+    }
+    const int u = pos & 3;
+    if (u == 0) {
+      const int k = aq();
+      if (k >= hq) refill();   // a step longer than the window (rare)
+      cur = slot(k);
+    }
+    ++pos;
+    uint32_t y = u == 0 ? cur.x : (u == 1 ? cur.y : (u == 2 ? cur.z : cur.w));
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  __device__ __forceinline__ static uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  // random_sample's two words at once: at an even position both words lie in
+  // one quad (words 0-1 or 2-3) and in one block (624 is even).  Only
+  // randint's single words make the position odd.
+  __device__ __forceinline__ double next_double() {
+    uint32_t wa, wb;
+    if (pos & 1) {
+      wa = next32();
+      wb = next32();
+    } else {
+      if (pos == kN) {
+        buf ^= 1;
+        pos = 0;
+        pend = 1;
+        ++blk;
+      }
+      const bool lo = (pos & 3) == 0;
+      if (lo) {
+        const int k = aq();
+        if (k >= hq) refill();   // a step longer than the window (rare)
+        cur = slot(k);
+      }
+      pos += 2;
+      wa = temper(lo ? cur.x : cur.z);
+      wb = temper(lo ? cur.y : cur.w);
+    }
+    const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+
+  __device__ __forceinline__ int packed() const {
+    return pos | (buf << 16) | (pend << 17);
+  }
 };
 
 // legacy_gauss: polar method, second deviate cached across calls
@@ -314,6 +531,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
   const int64_t rowlen = (int64_t)a.R * a.n;
   for (int64_t t = 0; t < a.n_steps; ++t) {
     double *row = a.out + t * rowlen + c;
+    m.maintain();   // wave-uniform: every active lane is here
     if (a.gibbs) {
       // rf.py:446-452: block (step0 + t) mod ceil(d / tsteps) of the cycle
       const int64_t nblk = (a.d + a.R - 1) / a.R;
@@ -346,6 +564,10 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       // r2) then runs over the step's pairs as independent chains.  The
       // draws, their order, the arithmetic and the cached deviate are
       // legacy_gauss's exactly.
+      // every chain draws d normals per step from the same start, so the
+      // cached-deviate flag is the same in every lane: made wave-uniform, the
+      // row indices order[j] below are scalar loads
+      has = __builtin_amdgcn_readfirstlane(has);
       int j0 = 0;
       if (has) {
         row[(int64_t)a.order[0] * a.n] = gauss;
@@ -419,6 +641,36 @@ __global__ __launch_bounds__(256) void legacy_gen_db_kernel(LegacyArgs a) {
   a.pos[c] = m.packed();
 }
 
+// The windowed generator (Mt3): dynamic LDS = the lanes' rings (2H quads
+// each) followed by the polar stage ((d + 1) / 2 pairs each).
+template <int H>
+__global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void legacy_gen_win_kernel(LegacyArgs a) {
+  extern __shared__ w4 s_lw[];
+  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
+  if (c >= a.n) return;
+  Mt3<H> m;
+  m.key = reinterpret_cast<w4 *>(a.key);
+  m.n = a.n;
+  m.c = c;
+  m.init(a.pos[c], s_lw + threadIdx.x);
+  legacy_gen_body(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy));
+  a.pos[c] = m.packed();
+}
+
+template <int H>
+hipError_t launch_win(const LegacyArgs &a, hipStream_t s) {
+  const int pairs = a.normal ? (a.d + 1) / 2 : 0;
+  const size_t lds = (size_t)(2 * H + pairs) * kBlockLegacy * sizeof(uint4);
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&legacy_gen_win_kernel<H>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  const dim3 grid((unsigned)((a.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+  hipLaunchKernelGGL(legacy_gen_win_kernel<H>, grid, block, lds, s, a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
@@ -435,6 +687,11 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
 }
 
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
+  if (a.db && a.win) {
+    // 2H = 32 quads (128 words) per lane while the stage leaves room
+    if (!a.normal || a.d <= 12) return launch_win<16>(a, s);
+    return launch_win<8>(a, s);
+  }
   const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
   if (a.db)
     hipLaunchKernelGGL(legacy_gen_db_kernel, grid, block, 0, s, a);

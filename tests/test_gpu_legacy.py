@@ -69,7 +69,7 @@ def _check(dev, ref, normal_rows):
   for j in range(ref.shape[1]):
     if j in normal_rows:
       rel = np.abs(dev[:, j] - ref[:, j]) / np.maximum(np.abs(ref[:, j]), 1e-300)
-      assert rel.max() <= 4e-16, (j, rel.max())
+      assert rel.max() <= 6e-16, (j, rel.max())   # the device log: <= 2 ulp
       assert np.mean(dev[:, j] == ref[:, j]) > 0.98
     else:
       np.testing.assert_array_equal(dev[:, j], ref[:, j])
@@ -131,3 +131,31 @@ def test_full_width_cfg2_replay_on_device_streams():
   assert np.max(np.abs(out['v_x'][pick] - ref['v_x']) / den) <= 1e-12
   den = np.maximum(np.abs(ref['v_p']), np.finfo(float).tiny)
   assert np.max(np.abs(out['v_p'][pick] - ref['v_p']) / den) <= 1e-12
+
+
+@pytest.mark.parametrize('name', ['diag10', 'uniform10', 'randint_wide', 'gauss5_permuted'])
+def test_device_streams_many_short_launches(name):
+  """Launch boundaries at every phase of the LDS window and of the
+  double-buffered state (mid-quad positions, block ends, pending refills):
+  launches of 1, 2, 3, 5, ... steps in a row equal one RandomState stream,
+  and so does one long launch spanning several 624-word blocks."""
+  spec = _specs()[name]
+  n = 80
+  seeds = np.arange(5000, 5000 + n)
+  sizes = [1, 2, 3, 5, 8, 13, 21, 34, 1, 1, 40]
+  eng = _engine(spec, n, seeds)
+  parts = []
+  for t in sizes:
+    eng.legacy_replay(t)
+    parts.append(eng.get_replay(0, t))
+  eng.close()
+  total = sum(sizes)
+  ref = oracle.legacy_streams(spec, seeds, total)
+  d = int(spec['dim'])
+  normal = set(range(d)) if spec['proposal']['kind'] == 'gauss' else set()
+  _check(np.concatenate(parts), ref, normal)
+  eng = _engine(spec, n, seeds)
+  eng.legacy_replay(total)
+  one = eng.get_replay(0, total)
+  eng.close()
+  _check(one, ref, normal)
