@@ -366,6 +366,25 @@ __device__ __forceinline__ void st_buf(double *base, uint32_t voff,
                                         (int)voff, (int)soff, 2);
 }
 
+// 16-bit store through a buffer resource (accept words of the 16-chain
+// kernels); base wave-uniform as in st_buf.
+__device__ __forceinline__ void st_buf16(void *base, uint32_t voff, uint16_t v) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b16(v, rs, (int)voff, 0, 0);
+}
+
+// A pointer the compiler cannot prove wave-uniform but that is: its
+// first lane's value in SGPRs, so that a buffer resource built from it is
+// scalar (no waterfall loop around the store).
+template <typename T>
+__device__ __forceinline__ T *wave_uniform(T *p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return reinterpret_cast<T *>(((uint64_t)hi << 32) | lo);
+}
+
 // Legacy fp32 normals (PBH_RNG_PHILOX_FP32, the round-1 production form, kept
 // as a labelled comparison): two standard-normal pairs per Philox
 // block from the hardware fp32 transcendentals (v_log_f32, v_sin_f32,

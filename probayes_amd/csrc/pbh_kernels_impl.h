@@ -1238,10 +1238,11 @@ __device__ __forceinline__ Decision accept_filter_ms(double Mp, double Sp,
                   ((float)Sp * __builtin_amdgcn_rcpf((float)S));
   const float tlo = (float)lead * w;
   const float thi = tlo + w;
-  const bool inr = __builtin_fabs(Mp) <= 698. && __builtin_fabs(M) <= 698.;
+  // bitwise & / |: evaluated branch-free (no exec-masked region around e)
+  const bool inr = (__builtin_fabs(Mp) <= 698.) & (__builtin_fabs(M) <= 698.);
   const bool af = thi <= e * 0.999996f;
   const bool rf = tlo > e * 1.000004f;
-  return Decision{inr && af, !(inr && (af || rf))};
+  return Decision{(bool)(inr & af), !(inr & (af | rf))};
 }
 
 template <int D, int K, int L>
@@ -1488,6 +1489,26 @@ __device__ __forceinline__ Decision accept_filter_ms32(double Mp, float Sp,
   return Decision{inr && af, !(inr && (af || rf))};
 }
 
+// The same decision with the proposal's terms taken relative to the STATE's
+// max lm instead of its own: e = sum_k exp2f(fp32((v'_k - lm) log2 e)) x
+// rcp(fp32(S)), S the state's sum relative to lm.  The proposal's max M' (two
+// DPP rounds) is then off the decision's dependency chain.  Where a decision
+// can hinge on e (e <= 1: every term 2^y <= K, y <= 2; terms below 2^-15 do
+// not matter at the 4e-6 margin) |y| <= 17: argument rounding 4.2e-8 x 17 =
+// 7.1e-7 + 1 ulp per term, the sum within 1.1e-6, rcp and the conversion of S
+// 1.8e-7: about 1.4e-6 < 4e-6.  e = inf (a far better proposal) accepts;
+// e = 0 with lead 0 is undecided.  inr: |M'|, |lm| <= 698 as before.
+template <int LB>
+__device__ __forceinline__ Decision accept_filter_rel32(float e, bool inr,
+                                                        uint32_t lead) {
+  constexpr float w = 1.0f / (float)(1u << LB);
+  const float tlo = (float)lead * w;
+  const float thi = tlo + w;
+  const bool af = thi <= e * 0.999996f;
+  const bool rf = tlo > e * 1.000004f;
+  return Decision{(bool)(inr & af), !(inr & (af | rf))};
+}
+
 template <int CTRL>
 __device__ __forceinline__ float qperm_f32(float v) {
   return __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_mov_dpp(
@@ -1548,11 +1569,12 @@ void mh_gmm_quad_kernel(KArgs a) {
   for (int i = 0; i < D; ++i) x[i] = a.x[i * a.n + cc];
   const double lp0 = a.lp[cc];
   double lm = lp0, ls = 1.0;   // the state's density as (M, S): lp = M + ln S
-  float ls32 = 1.0f;           // S of the state in fp32 (the decision path)
+  float lr32 = 1.0f;           // 1 / fp32(S) of the state (the decision path)
   int64_t nacc = 0;
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
   const uint32_t xoff = (uint32_t)(((int64_t)(p % D) * a.n + cc) * 8);
+  const uint32_t lpoff = (uint32_t)(((int64_t)p * a.n + cc) * 8);   // FULL
   double *txrow = a.tx + ri * D * a.n;   // record ri's rows (wave-uniform)
   const int64_t rstride = (int64_t)D * a.n;
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
@@ -1595,20 +1617,24 @@ void mh_gmm_quad_kernel(KArgs a) {
         const double u = (xp[i] - cmu[i]) * cw;
         v = __builtin_fma(-u, u, v);
       }
+      // decision path: the terms relative to the state's max lm
+      // (accept_filter_rel32).  A lane p >= K holds v = -inf: its terms are
+      // exp(-inf) = 0 in both paths without a select (exp_tab clamps at -746:
+      // 0 to within 2^-1074)
+      float e32 = __builtin_amdgcn_exp2f((float)((v - lm) * 1.4426950408889634));
+      e32 = e32 + qperm_f32<kQuadXor1>(e32);
+      const float E32 = (e32 + qperm_f32<kQuadXor2>(e32)) * lr32;
+      // record path (off the decision's chain): M' and S in fp64
       double M = __builtin_fmax(v, qperm_f64<kQuadXor1>(v));
       M = __builtin_fmax(M, qperm_f64<kQuadXor2>(M));
       const double dv = v - M;
-      // decision path: S in fp32 from v_exp_f32 (accept_filter_ms32)
-      float e32 = own ? __builtin_amdgcn_exp2f((float)(dv * 1.4426950408889634)) : 0.f;
-      e32 = e32 + qperm_f32<kQuadXor1>(e32);
-      const float S32 = e32 + qperm_f32<kQuadXor2>(e32);
-      // record path (off the decision's chain): S in fp64
-      double e = own ? exp_tab(dv, s_bmt) : 0.;
+      const bool inr = (__builtin_fabs(M) <= 698.) & (__builtin_fabs(lm) <= 698.);
+      double e = exp_tab(dv, s_bmt);
       e = e + qperm_f64<kQuadXor1>(e);
       const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
       bool acc;
       if constexpr (FULL) {
-        const Decision dc = accept_filter_ms32<LB>(M, S32, lm, ls32, lead);
+        const Decision dc = accept_filter_rel32<LB>(E32, inr, lead);
         acc = dc.acc;
         if (__ballot(dc.need)) {   // wave-uniform, rare
           if (dc.need) acc = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
@@ -1617,7 +1643,7 @@ void mh_gmm_quad_kernel(KArgs a) {
         acc = true;                                  // s = None on step 1
       } else {
         const Decision dc = a.acc_beta == 1.0
-            ? accept_filter_ms32<LB>(M, S32, lm, ls32, lead)
+            ? accept_filter_rel32<LB>(E32, inr, lead)
             : accept_filter_lead<LB>((M + ln_tab(S, s_bmt)) * a.acc_beta,
                                      (lm + ln_tab(ls, s_bmt)) * a.acc_beta,
                                      lead, false);
@@ -1636,7 +1662,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
       lm = acc ? M : lm;
       ls = acc ? S : ls;
-      ls32 = acc ? S32 : ls32;
+      lr32 = acc ? __builtin_amdgcn_rcpf((float)S) : lr32;
       gm[j] = lm;
       gs[j] = ls;
       if constexpr (MOM) {
@@ -1651,7 +1677,9 @@ void mh_gmm_quad_kernel(KArgs a) {
         double xo = x[0];
 #pragma unroll
         for (int i = 1; i < D; ++i) xo = p % D == i ? x[i] : xo;
-        st_buf(txrow, xoff, 0, xo);
+        // the record row is wave-uniform: a scalar buffer resource (without
+        // readfirstlane the compiler wraps the store in a waterfall loop)
+        st_buf(wave_uniform(txrow), xoff, 0, xo);
         grec[j] = ri;
         uint64_t m = __ballot(acc) & 0x1111111111111111ull & act_bits;
         m = (m | (m >> 3)) & 0x0303030303030303ull;
@@ -1659,7 +1687,7 @@ void mh_gmm_quad_kernel(KArgs a) {
         m = (m | (m >> 12)) & 0x000000FF000000FFull;
         m = (m | (m >> 24)) & 0xFFFFull;
         // every lane stores the wave's word (one address, one value)
-        reinterpret_cast<uint16_t *>(a.tacc)[ri * 4 * a.W + wave] = (uint16_t)m;
+        st_buf16(wave_uniform(a.tacc + ri * a.W), (uint32_t)(wave * 2), (uint16_t)m);
         ++ri;
         txrow += rstride;
         return;
@@ -1704,7 +1732,11 @@ void mh_gmm_quad_kernel(KArgs a) {
       pss = p == j ? gs[j] : pss;
       prec = p == j ? grec[j] : prec;
     }
-    if (FULL || (prec >= 0 && active)) {
+    if constexpr (FULL) {
+      // records ri - 4 .. ri - 1 (lane p: step 4 G + p): a uniform base
+      const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
+      st_buf(wave_uniform(a.tlp + (ri - 4) * a.n), lpoff, 0, lpr);
+    } else if (prec >= 0 && active) {
       const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
       __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + cc]);
     }
