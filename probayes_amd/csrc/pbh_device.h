@@ -366,6 +366,29 @@ __device__ __forceinline__ void st_buf(double *base, uint32_t voff,
                                         (int)voff, (int)soff, 2);
 }
 
+// Lane selects in the VOP3 (e64) encoding.  On gfx950 the VOP2 form
+// v_cndmask_b32_e32 (mask implicitly in VCC), which the compiler picks
+// whenever the condition sits in VCC, issues at ~23 cycles per wave
+// instruction at any occupancy, against ~5 for the e64 form reading the same
+// mask -- VCC included (tools/ubench/isa_cost.hip, profiles/r02y_isa_cnd.txt).
+// These helpers pin the e64 form: m is the lane mask (a ballot of the
+// condition; inactive lanes' bits do not matter).
+__device__ __forceinline__ uint32_t sel_u32(uint64_t m, uint32_t if0, uint32_t if1) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+  return r;
+}
+__device__ __forceinline__ double sel_f64(uint64_t m, double if0, double if1) {
+  const uint64_t a = __builtin_bit_cast(uint64_t, if0), b = __builtin_bit_cast(uint64_t, if1);
+  const uint32_t lo = sel_u32(m, (uint32_t)a, (uint32_t)b);
+  const uint32_t hi = sel_u32(m, (uint32_t)(a >> 32), (uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float sel_f32(uint64_t m, float if0, float if1) {
+  return __builtin_bit_cast(float, sel_u32(m, __builtin_bit_cast(uint32_t, if0),
+                                           __builtin_bit_cast(uint32_t, if1)));
+}
+
 // 16-bit store through a buffer resource (accept words of the 16-chain
 // kernels); base wave-uniform as in st_buf.
 __device__ __forceinline__ void st_buf16(void *base, uint32_t voff, uint16_t v) {

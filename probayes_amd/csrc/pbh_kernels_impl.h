@@ -1072,11 +1072,12 @@ void mh_pair_kernel(KArgs a) {
     // half 1's decision is the chain's: lanes l and l + 32 both take bit
     // l + 32 of the ballot (SGPR mask ops; inverse_ballot feeds v_cndmask)
     const uint64_t mhi = __ballot(hi && acc) & 0xFFFFFFFF00000000ull;
-    const bool accl = __builtin_amdgcn_inverse_ballot_w64(mhi | (mhi >> 32));
+    const uint64_t macc = mhi | (mhi >> 32);   // lane mask of the chain's decision
+    const bool accl = __builtin_amdgcn_inverse_ballot_w64(macc);
 #pragma unroll
-    for (int i = 0; i < H; ++i) x[i] = accl ? xp[i] : x[i];
-    if (REPLAY) eB = accl ? eA : eB;
-    lp = accl ? lpp : lp;
+    for (int i = 0; i < H; ++i) x[i] = sel_f64(macc, x[i], xp[i]);
+    if (REPLAY) eB = sel_f64(macc, eB, eA);
+    lp = sel_f64(macc, lp, lpp);
     if constexpr (mom) {
       nacc += accl ? 1 : 0;
 #pragma unroll

@@ -4,6 +4,7 @@
 // Used to price the MH step's instruction mix.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstring>
 #include <cstdint>
 
 constexpr int R = 2048;
@@ -121,6 +122,54 @@ __global__ void k_cnd_vcc(uint32_t *out, uint32_t s) {
   for (int j = 0; j < 8; ++j) x ^= v[j];
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
+// e64 encoding reading VCC itself
+__global__ void k_cnd_e64_vcc(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a), "v"(s) : "vcc");
+  for (int i = 0; i < R; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(v[j]) : "v"(a) : );
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+// the kernel's pattern: a SALU op writes the mask, then 8 selects read it
+// (vcc / e32 against an SGPR pair / e64)
+__global__ void k_cnd_salu_vcc(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  const uint64_t m = 0x5555555555555555ull ^ s;
+  for (int i = 0; i < R; ++i) {
+    asm volatile("s_mov_b64 vcc, %0" :: "s"(m) : "vcc");
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(v[j]) : "v"(a) : );
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ void k_cnd_salu_sgpr(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  uint64_t m = 0x5555555555555555ull ^ s;
+  for (int i = 0; i < R; ++i) {
+    uint64_t mm;
+    asm volatile("s_mov_b64 %0, %1" : "=s"(mm) : "s"(m));
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(v[j]) : "v"(a), "s"(mm));
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
 // cmp + cndmask pair as the compiler emits a select (v_cmp -> s[..] -> cndmask)
 __global__ void k_sel(uint32_t *out, uint32_t s) {
   uint32_t v[8];
@@ -171,7 +220,7 @@ double cyc(K k, uint32_t *buf, int wps) {
   return ms / 4 * 1e-3 * 2.4e9 / per_simd;
 }
 
-int main() {
+int main(int argc, char **argv) {
   uint32_t *u;
   hipMalloc(&u, 256 * 8 * 256 * 4);
   struct E { const char *n; void (*k)(uint32_t *, uint32_t); };
@@ -190,11 +239,14 @@ int main() {
       {"v_lshl_add_u64", k_lshladd64}, {"v_pk_fma_f32", k_pkfma32},
       {"v_mov_b64", k_mov64}, {"v_cndmask_e64(sgpr)", k_cnd_sgpr},
       {"v_cndmask_e32(vcc)", k_cnd_vcc}, {"select(cmp+cnd)/2", k_sel},
+      {"v_cndmask_e64(vcc)", k_cnd_e64_vcc}, {"s_mov vcc+8 e32(vcc)", k_cnd_salu_vcc},
+      {"s_mov sgpr+8 e64(sgpr)", k_cnd_salu_sgpr},
       {"LAT v_fma_f64", k_fma64_lat}, {"LAT v_xor_b32", k_xor_lat},
       {"LAT v_mad_u64_u32", k_mad64_lat}};
   printf("%-24s %8s %8s %8s %8s\n", "instruction", "1w/SIMD", "2w/SIMD",
          "4w/SIMD", "8w/SIMD");
   for (const E &e : es) {
+    if (argc > 1 && !strstr(e.n, argv[1])) continue;
     printf("%-24s", e.n);
     for (int w : {1, 2, 4, 8}) printf(" %8.2f", cyc(e.k, u, w));
     printf("\n");
