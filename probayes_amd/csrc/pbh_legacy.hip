@@ -265,6 +265,88 @@ struct Mt2 {
 // of HIP's uint4 struct stayed in scratch)
 typedef uint32_t w4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ void mt3_twist(w4 *key, int64_t n, int64_t c, int s) {
+  auto q = [&](int b, int i) -> w4 & { return key[((int64_t)b * kQ + i) * n + c]; };
+  constexpr int kTB = 14;   // twist batch (56 = 4 x 14, 98 = 7 x 14)
+  const int d = s ^ 1;
+  for (int i0 = 0; i0 < 56; i0 += kTB) {
+    w4 a[kTB + 1], h[kTB + 1];
+#pragma unroll
+    for (int u = 0; u <= kTB; ++u) {
+      a[u] = q(s, i0 + u);
+      h[u] = q(s, i0 + 99 + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kTB; ++u) {
+      w4 o;
+      o.x = h[u].y ^ mt_f(a[u].x, a[u].y);
+      o.y = h[u].z ^ mt_f(a[u].y, a[u].z);
+      o.z = h[u].w ^ mt_f(a[u].z, a[u].w);
+      o.w = h[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+      q(d, i0 + u) = o;
+    }
+  }
+  {                                          // quad 56: words 224 .. 227
+    const w4 a = q(s, 56), nx = q(s, 57), h = q(s, 155), d0 = q(d, 0);
+    w4 o;
+    o.x = h.y ^ mt_f(a.x, a.y);              // src[621]
+    o.y = h.z ^ mt_f(a.y, a.z);              // src[622]
+    o.z = h.w ^ mt_f(a.z, a.w);              // src[623]
+    o.w = d0.x ^ mt_f(a.w, nx.x);            // dst[0]
+    q(d, 56) = o;
+  }
+  for (int i0 = 57; i0 < kQ - 1; i0 += kTB) {
+    w4 a[kTB + 1], l[kTB + 1];
+#pragma unroll
+    for (int u = 0; u <= kTB; ++u) {
+      a[u] = q(s, i0 + u);
+      l[u] = q(d, i0 - 57 + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kTB; ++u) {
+      w4 o;
+      o.x = l[u].y ^ mt_f(a[u].x, a[u].y);
+      o.y = l[u].z ^ mt_f(a[u].y, a[u].z);
+      o.z = l[u].w ^ mt_f(a[u].z, a[u].w);
+      o.w = l[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+      q(d, i0 + u) = o;
+    }
+  }
+  {                                          // quad 155: words 620 .. 623
+    const w4 a = q(s, kQ - 1), d0 = q(d, 0), d98 = q(d, 98), d99 = q(d, 99);
+    w4 o;
+    o.x = d98.y ^ mt_f(a.x, a.y);            // dst[393]
+    o.y = d98.z ^ mt_f(a.y, a.z);            // dst[394]
+    o.z = d98.w ^ mt_f(a.z, a.w);            // dst[395]
+    o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
+    q(d, kQ - 1) = o;
+  }
+}
+
+// Mt3's rare refills (a launch's first two, and a step longer than the
+// window) out of line, with plain values in and out so that the generator's
+// state never has to live in memory; the step-top refill stays inline.
+template <int H>
+__device__ __attribute__((noinline)) int mt3_refill_cold(w4 *key, int64_t n, int64_t c,
+                                                         w4 *win, int hq, int blk,
+                                                         int buf, int pend) {
+  const int nb = (blk + 1) * kQ;
+  if (pend && hq + H > nb) {   // the head enters the next block
+    mt3_twist(key, n, c, buf);
+    pend = 0;
+  }
+  w4 v[H];
+#pragma unroll
+  for (int u = 0; u < H; ++u) {
+    const int k = hq + u;
+    const bool nx = k >= nb;
+    v[u] = key[((int64_t)(buf ^ (nx ? 1 : 0)) * kQ + (nx ? k - nb : k - blk * kQ)) * n + c];
+  }
+#pragma unroll
+  for (int u = 0; u < H; ++u) win[((hq + u) & (2 * H - 1)) * kBlockLegacy] = v[u];
+  return pend;
+}
+
 template <int H>
 struct Mt3 {
   static constexpr bool kLockstep = true;
@@ -287,69 +369,12 @@ struct Mt3 {
   }
   __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
 
-  __device__ __forceinline__ void twist_from(int s) {
-    const int d = s ^ 1;
-    for (int i0 = 0; i0 < 56; i0 += kTB) {
-      w4 a[kTB + 1], h[kTB + 1];
-#pragma unroll
-      for (int u = 0; u <= kTB; ++u) {
-        a[u] = q(s, i0 + u);
-        h[u] = q(s, i0 + 99 + u);
-      }
-#pragma unroll
-      for (int u = 0; u < kTB; ++u) {
-        w4 o;
-        o.x = h[u].y ^ mt_f(a[u].x, a[u].y);
-        o.y = h[u].z ^ mt_f(a[u].y, a[u].z);
-        o.z = h[u].w ^ mt_f(a[u].z, a[u].w);
-        o.w = h[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
-        q(d, i0 + u) = o;
-      }
-    }
-    {                                          // quad 56: words 224 .. 227
-      const w4 a = q(s, 56), nx = q(s, 57), h = q(s, 155), d0 = q(d, 0);
-      w4 o;
-      o.x = h.y ^ mt_f(a.x, a.y);              // src[621]
-      o.y = h.z ^ mt_f(a.y, a.z);              // src[622]
-      o.z = h.w ^ mt_f(a.z, a.w);              // src[623]
-      o.w = d0.x ^ mt_f(a.w, nx.x);            // dst[0]
-      q(d, 56) = o;
-    }
-    for (int i0 = 57; i0 < kQ - 1; i0 += kTB) {
-      w4 a[kTB + 1], l[kTB + 1];
-#pragma unroll
-      for (int u = 0; u <= kTB; ++u) {
-        a[u] = q(s, i0 + u);
-        l[u] = q(d, i0 - 57 + u);
-      }
-#pragma unroll
-      for (int u = 0; u < kTB; ++u) {
-        w4 o;
-        o.x = l[u].y ^ mt_f(a[u].x, a[u].y);
-        o.y = l[u].z ^ mt_f(a[u].y, a[u].z);
-        o.z = l[u].w ^ mt_f(a[u].z, a[u].w);
-        o.w = l[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
-        q(d, i0 + u) = o;
-      }
-    }
-    {                                          // quad 155: words 620 .. 623
-      const w4 a = q(s, kQ - 1), d0 = q(d, 0), d98 = q(d, 98), d99 = q(d, 99);
-      w4 o;
-      o.x = d98.y ^ mt_f(a.x, a.y);            // dst[393]
-      o.y = d98.z ^ mt_f(a.y, a.z);            // dst[394]
-      o.z = d98.w ^ mt_f(a.z, a.w);            // dst[395]
-      o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
-      q(d, kQ - 1) = o;
-    }
-  }
+  __device__ __forceinline__ void twist_from(int s) { mt3_twist(key, n, c, s); }
 
   // quads hq .. hq + H - 1 into the ring (their slots' quads are consumed)
+  // the step-top refill: maintain() has twisted the next block already
   __device__ __forceinline__ void refill() {
     const int nb = (blk + 1) * kQ;   // first quad of the next block
-    if (pend && hq + H > nb) {       // the head enters the next block
-      twist_from(buf);
-      pend = 0;
-    }
     w4 v[H];
 #pragma unroll
     for (int u = 0; u < H; ++u) {
@@ -359,6 +384,11 @@ struct Mt3 {
     }
 #pragma unroll
     for (int u = 0; u < H; ++u) slot(hq + u) = v[u];
+    hq += H;
+  }
+
+  __device__ __forceinline__ void refill_cold() {
+    pend = mt3_refill_cold<H>(key, n, c, win, hq, blk, buf, pend);
     hq += H;
   }
 
@@ -373,14 +403,17 @@ struct Mt3 {
       pend = 0;
     }
     hq = pos >> 2;
-    refill();
-    refill();
+    refill_cold();
+    refill_cold();
     if (pos & 3) cur = slot(aq());
   }
 
   // wave-uniform point (top of a step): the refill twist, then the window
   __device__ __forceinline__ void maintain() {
-    if (__builtin_amdgcn_ballot_w64(pend && pos >= kRefill)) {
+    // the refill twist: at word 312, or earlier when the head's next refill
+    // enters the next block
+    const bool due = pend && (pos >= kRefill || hq + H > (blk + 1) * kQ);
+    if (__builtin_amdgcn_ballot_w64(due)) {
       if (pend) {   // every pending lane: its free buffer holds a consumed block
         twist_from(buf);
         pend = 0;
@@ -401,7 +434,7 @@ struct Mt3 {
     const int u = pos & 3;
     if (u == 0) {
       const int k = aq();
-      if (k >= hq) refill();   // a step longer than the window (rare)
+      if (k >= hq) refill_cold();   // a step longer than the window (rare)
       cur = slot(k);
     }
     ++pos;
@@ -439,7 +472,7 @@ struct Mt3 {
       const bool lo = (pos & 3) == 0;
       if (lo) {
         const int k = aq();
-        if (k >= hq) refill();   // a step longer than the window (rare)
+        if (k >= hq) refill_cold();   // a step longer than the window (rare)
         cur = slot(k);
       }
       pos += 2;
@@ -523,16 +556,23 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
   has_gauss[c] = 0;
 }
 
-template <class M>
+// MODE: -1 any (runtime flags), else the one path a kernel compiles
+// (kModeGibbs, kModeVardelta, kModeNormal, kModeRaw) -- one path per kernel
+// keeps each function small (isa_e64.py rewrites only functions < 128 KB).
+constexpr int kModeAny = -1, kModeGibbs = 0, kModeVardelta = 1, kModeNormal = 2,
+              kModeRaw = 3;
+
+template <class M, int MODE = kModeAny>
 __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m,
                                                 double2 *stage = nullptr) {
+  constexpr bool kAny = MODE == kModeAny;
   double gauss = a.gauss[c];
   int has = a.has_gauss[c];
   const int64_t rowlen = (int64_t)a.R * a.n;
   for (int64_t t = 0; t < a.n_steps; ++t) {
     double *row = a.out + t * rowlen + c;
     m.maintain();   // wave-uniform: every active lane is here
-    if (a.gibbs) {
+    if ((kAny || MODE == kModeGibbs) && (!kAny || a.gibbs)) {
       // rf.py:446-452: block (step0 + t) mod ceil(d / tsteps) of the cycle
       const int64_t nblk = (a.d + a.R - 1) / a.R;
       const int cm = (int)(((a.step0 + t) % nblk) * a.R);
@@ -541,7 +581,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
         row[(int64_t)j * a.n] = j < cnt ? m.next_double() : __builtin_nan("");
       continue;
     }
-    if (a.vardelta) {
+    if ((kAny || MODE == kModeVardelta) && (!kAny || a.vardelta)) {
       // Field.eval_delta draws per variable in key order (variable.py:618-633)
       for (int j = 0; j < a.d; ++j) {
         const int md = (int)((a.vmode >> (2 * j)) & 3u);
@@ -555,7 +595,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
       continue;
     }
-    if (M::kLockstep && a.normal) {
+    if (M::kLockstep && (kAny || MODE == kModeNormal) && (!kAny || a.normal)) {
       // the step's d polar-method normals.  Lanes run the ATTEMPTS in
       // lockstep (one per iteration until each holds its pairs: a wave loops
       // ~max over lanes of the step's attempts, about 9.5 for 5 pairs, not
@@ -608,8 +648,9 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
       continue;
     }
+    if constexpr (!kAny && MODE != kModeRaw) continue;   // not reached
     for (int j = 0; j < a.d; ++j) {
-      const double v = a.normal ? legacy_gauss(m, gauss, has) : m.next_double();
+      const double v = (kAny && a.normal) ? legacy_gauss(m, gauss, has) : m.next_double();
       row[(int64_t)a.order[j] * a.n] = v;    // draw j feeds dim order[j]
     }
     row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
@@ -643,7 +684,7 @@ __global__ __launch_bounds__(256) void legacy_gen_db_kernel(LegacyArgs a) {
 
 // The windowed generator (Mt3): dynamic LDS = the lanes' rings (2H quads
 // each) followed by the polar stage ((d + 1) / 2 pairs each).
-template <int H>
+template <int H, int MODE>
 __global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void legacy_gen_win_kernel(LegacyArgs a) {
   extern __shared__ w4 s_lw[];
@@ -654,21 +695,29 @@ void legacy_gen_win_kernel(LegacyArgs a) {
   m.n = a.n;
   m.c = c;
   m.init(a.pos[c], s_lw + threadIdx.x);
-  legacy_gen_body(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy));
+  legacy_gen_body<Mt3<H>, MODE>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy));
   a.pos[c] = m.packed();
+}
+
+template <int H, int MODE>
+hipError_t launch_win_mode(const LegacyArgs &a, hipStream_t s) {
+  const int pairs = a.normal ? (a.d + 1) / 2 : 0;
+  const size_t lds = (size_t)(2 * H + pairs) * kBlockLegacy * sizeof(uint4);
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&legacy_gen_win_kernel<H, MODE>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  const dim3 grid((unsigned)((a.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+  hipLaunchKernelGGL((legacy_gen_win_kernel<H, MODE>), grid, block, lds, s, a);
+  return hipGetLastError();
 }
 
 template <int H>
 hipError_t launch_win(const LegacyArgs &a, hipStream_t s) {
-  const int pairs = a.normal ? (a.d + 1) / 2 : 0;
-  const size_t lds = (size_t)(2 * H + pairs) * kBlockLegacy * sizeof(uint4);
-  hipError_t err = hipFuncSetAttribute(
-      reinterpret_cast<const void *>(&legacy_gen_win_kernel<H>),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return err;
-  const dim3 grid((unsigned)((a.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
-  hipLaunchKernelGGL(legacy_gen_win_kernel<H>, grid, block, lds, s, a);
-  return hipGetLastError();
+  if (a.gibbs) return launch_win_mode<H, kModeGibbs>(a, s);
+  if (a.vardelta) return launch_win_mode<H, kModeVardelta>(a, s);
+  if (a.normal) return launch_win_mode<H, kModeNormal>(a, s);
+  return launch_win_mode<H, kModeRaw>(a, s);
 }
 
 }  // namespace
