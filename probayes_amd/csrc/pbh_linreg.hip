@@ -226,34 +226,142 @@ linreg_gibbs_kernel(LinregK a) {
   a.lp_state[c] = lp;
 }
 
-// FAST arithmetic of one step (the same expressions as the FAST branches of
-// linreg_gibbs_kernel, so both kernels give identical chains).
-__device__ __forceinline__ void fast_step(const LinregK &a, int key, double z,
-                                          double nd, double &b0, double &b1,
-                                          double &sg, double &lp) {
-  if (key == 2) {
-    const double cb = a.beta + 0.5 * fast_ss(a, nd, b0, b1);
-    sg = 1.0 / sqrt((1.0 / cb) * z);
-  } else {
-    const double yp = 1.0 / (sg * sg);
-    if (key == 0) {
-      const double v = 1.0 / (a.p0 + nd * yp);
-      const double s = nd * (a.ybar - b1 * a.xbar);
-      const double m = (a.p0 * a.m0 + yp * s) * v;
-      b0 = m + sqrt(v) * z;
-    } else {
-      const double v = 1.0 / (a.p1 + yp * a.sxx);
-      const double s = __builtin_fma(nd * a.xbar, a.ybar - b0, a.cxy);
-      const double m = (a.p1 * a.m1 + yp * s) * v;
-      b1 = m + sqrt(v) * z;
-    }
+// FAST arithmetic (PHILOX): no IEEE divisions or square roots on the step's
+// dependency chain -- reciprocals and inverse square roots from v_rcp_f64 /
+// v_rsq_f64 with two Newton steps (within an ulp or two of the IEEE forms; the
+// FAST chain is a production form, checked against the reference arithmetic
+// to 1e-9 in tests/test_linreg.py):
+//   beta_k:  P = p_k + yp S_k,  r = P^-1/2,  b_k = (p_k m_k + yp s) r^2 + r z
+//            (v = 1/P and sqrt(v) = r of cond_reg);
+//   y_sigma: w = z / cb,  sg = w^-1/2  (1/sqrt((1/cb) z));
+//   v.prob:  -ss yp / 2 - n (logC + log sg),  yp = 1/sg^2.
+// yp and log sg are pure functions of sg (cached between y_sigma steps and
+// recomputed at launch entry), so launch splits give identical chains.
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+  return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * __builtin_fma(-hx * y, y, 1.5);
+  return y * __builtin_fma(-hx * y, y, 1.5);
+}
+
+struct FastState {
+  double b0, b1, sg, yp, lsg, lp;
+  __device__ __forceinline__ void set_sg(double s) {
+    sg = s;
+    yp = rcp_nr(s * s);
+    lsg = fast_log(s);
   }
-  const double lsg = fast_log(sg);
-  lp = -0.5 * fast_ss(a, nd, b0, b1) / (sg * sg) - nd * (a.logC + lsg);
-  const double q0 = (b0 >= a.lo0 && b0 <= a.hi0) ? a.pri0 : kNearlyNegInf;
-  const double q1 = (b1 >= a.lo1 && b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
-  const double q2 = (sg >= a.lo2 && sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
-  lp = ((lp + q0) + q1) + q2;
+};
+
+__device__ __forceinline__ void fast_step(const LinregK &a, int key, double z,
+                                          double nd, FastState &f) {
+  if (key == 2) {
+    const double cb = a.beta + 0.5 * fast_ss(a, nd, f.b0, f.b1);
+    f.set_sg(rsq_nr(z * rcp_nr(cb)));
+  } else if (key == 0) {
+    const double r = rsq_nr(__builtin_fma(nd, f.yp, a.p0));
+    const double s = nd * (a.ybar - f.b1 * a.xbar);
+    f.b0 = __builtin_fma(r, z, (a.p0 * a.m0 + f.yp * s) * (r * r));
+  } else {
+    const double r = rsq_nr(__builtin_fma(f.yp, a.sxx, a.p1));
+    const double s = __builtin_fma(nd * a.xbar, a.ybar - f.b0, a.cxy);
+    f.b1 = __builtin_fma(r, z, (a.p1 * a.m1 + f.yp * s) * (r * r));
+  }
+  double lp = __builtin_fma(-0.5 * fast_ss(a, nd, f.b0, f.b1), f.yp, -nd * (a.logC + f.lsg));
+  const double q0 = (f.b0 >= a.lo0 && f.b0 <= a.hi0) ? a.pri0 : kNearlyNegInf;
+  const double q1 = (f.b1 >= a.lo1 && f.b1 <= a.hi1) ? a.pri1 : kNearlyNegInf;
+  const double q2 = (f.sg >= a.lo2 && f.sg <= a.hi2) ? a.pri2 : kNearlyNegInf;
+  f.lp = ((lp + q0) + q1) + q2;
+}
+
+// Marsaglia-Tsang attempts 2.. of a cycle (attempt 1 is drawn up front with
+// the cycle's normal pair); the same blocks and tests as mt_gamma<false>.
+__device__ __attribute__((noinline)) double mt_gamma_tail(const LinregK &a, const BMTables *tb,
+                                                          int64_t gc, int64_t cycle,
+                                                          double out) {
+  const double d = a.alpha - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  for (uint32_t att = 2; att <= 64; ++att) {
+    double z, z1;
+    normal_pair<false>(draw_block(a, gc, cycle, att), tb, z, z1);
+    const double t = 1.0 + c * z;
+    if (t <= 0.0) continue;
+    const double v = t * t * t;
+    out = d * v;
+    const u32x4 w2 = draw_block(a, gc, cycle, att + 0x10000u);
+    const double u = 1.0 - u01(w2.x, w2.y);
+    const double z2 = z * z;
+    if (u < 1.0 - 0.0331 * (z2 * z2)) break;
+    if (fast_log(u) < 0.5 * z2 + d - d * v + d * fast_log(v)) break;
+  }
+  return out;
+}
+
+// A cycle's draws: the beta normals (block (cycle, 0)) and the y_sigma gamma,
+// whose first Marsaglia-Tsang attempt (blocks (cycle, 1), (cycle, 1 + 2^16))
+// is computed beside the normals (three independent Philox blocks, two
+// Box-Muller pairs); a rejected first attempt continues out of line.
+__device__ __forceinline__ void cycle_draws(const LinregK &a, const BMTables *tb,
+                                            int64_t gc, int64_t cycle, double cm,
+                                            double dg, double &z0, double &z1,
+                                            double &g) {
+  const u32x4 wn = draw_block(a, gc, cycle, 0u);
+  const u32x4 wg = draw_block(a, gc, cycle, 1u);
+  const u32x4 wu = draw_block(a, gc, cycle, 1u + 0x10000u);
+  double zg, zg1;
+  normal_pair<false>(wn, tb, z0, z1);
+  normal_pair<false>(wg, tb, zg, zg1);
+  const double t = 1.0 + cm * zg;
+  const double v = t * t * t;
+  const double u = 1.0 - u01(wu.x, wu.y);
+  const double z2 = zg * zg;
+  bool done = t > 0.0 && u < 1.0 - 0.0331 * (z2 * z2);
+  if (!done && t > 0.0) done = fast_log(u) < 0.5 * z2 + dg - dg * v + dg * fast_log(v);
+  g = dg * v;
+  if (!done) g = mt_gamma_tail(a, tb, gc, cycle, t > 0.0 ? dg * v : dg);
+}
+
+// PHILOX production kernel, one chain per lane: the draws of each 3-step
+// cycle come first (cycle_draws), then the cycle's O(1) updates (fast_step).
+__global__ void __launch_bounds__(kBlock)
+linreg_fast_kernel(LinregK a) {
+  __shared__ BMTables s_bmt;
+  bm_tables_init(&s_bmt);
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.n) return;
+  const int64_t gc = a.chain_offset + c;
+  const int64_t n = a.n;
+  FastState f;
+  f.b0 = a.state[c];
+  f.b1 = a.state[n + c];
+  f.set_sg(a.state[2 * n + c]);
+  f.lp = 0.;
+  const double nd = (double)a.n_obs;
+  const double dg = a.alpha - 1.0 / 3.0;
+  const double cm = 1.0 / sqrt(9.0 * dg);
+  double z0 = 0., z1 = 0., g = 0.;
+  for (int64_t t = 0; t < a.n_steps; ++t) {
+    const int64_t step = a.step0 + t;
+    const int key = (int)(step % 3);
+    if (key == 0 || t == 0) cycle_draws(a, &s_bmt, gc, step / 3, cm, dg, z0, z1, g);
+    fast_step(a, key, key == 0 ? z0 : (key == 1 ? z1 : g), nd, f);
+    if (a.tx) {
+      double *tx = a.tx + t * 3 * n;
+      __builtin_nontemporal_store(f.b0, tx + c);
+      __builtin_nontemporal_store(f.b1, tx + n + c);
+      __builtin_nontemporal_store(f.sg, tx + 2 * n + c);
+    }
+    if (a.tp) __builtin_nontemporal_store(f.lp, a.tp + t * n + c);
+  }
+  a.state[c] = f.b0;
+  a.state[n + c] = f.b1;
+  a.state[2 * n + c] = f.sg;
+  a.lp_state[c] = f.lp;
 }
 
 __device__ __forceinline__ void lr_halves(double v, double &lo, double &hi) {
@@ -273,7 +381,7 @@ __device__ __forceinline__ void lr_halves(double v, double &lo, double &hi) {
 // continue in mt_gamma.  Two v_permlane32_swap exchanges give every lane the
 // cycle's three draws; both halves then carry the O(1) state update and split
 // the stores (half 0: beta_0, beta_1; half 1: y_sigma, lp).  Draws and
-// arithmetic equal linreg_gibbs_kernel<false>'s, so the chains are identical.
+// arithmetic equal linreg_fast_kernel's, so the chains are identical.
 // Measured slower (1.60 vs 1.22 ms at 65 536 chains x 1 000 steps): the
 // gamma half diverges from the normal half and both halves repeat the fp64
 // update, which outweighs the second wavefront per SIMD.  Off by default
@@ -290,11 +398,15 @@ linreg_pair_kernel(LinregK a) {
   const int64_t cc = live ? c : 0;
   const int64_t gc = a.chain_offset + cc;
   const int64_t n = a.n;
-  double b0 = a.state[cc], b1 = a.state[n + cc], sg = a.state[2 * n + cc];
+  FastState f;
+  f.b0 = a.state[cc];
+  f.b1 = a.state[n + cc];
+  f.set_sg(a.state[2 * n + cc]);
+  f.lp = 0.;
   const double nd = (double)a.n_obs;
   const double d = a.alpha - 1.0 / 3.0;
   const double cm = 1.0 / sqrt(9.0 * d);
-  double lp = 0., z0 = 0., z1 = 0., g = 0.;
+  double z0 = 0., z1 = 0., g = 0.;
   for (int64_t t = 0; t < a.n_steps; ++t) {
     const int64_t step = a.step0 + t;
     const int key = (int)(step % 3);
@@ -341,25 +453,25 @@ linreg_pair_kernel(LinregK a) {
       (void)hi_w;
     }
     const double z = key == 0 ? z0 : (key == 1 ? z1 : g);
-    fast_step(a, key, z, nd, b0, b1, sg, lp);
+    fast_step(a, key, z, nd, f);
     if (live) {
       if (!hi && a.tx) {
         double *tx = a.tx + t * 3 * n;
-        __builtin_nontemporal_store(b0, tx + c);
-        __builtin_nontemporal_store(b1, tx + n + c);
+        __builtin_nontemporal_store(f.b0, tx + c);
+        __builtin_nontemporal_store(f.b1, tx + n + c);
       } else if (hi) {
-        if (a.tx) __builtin_nontemporal_store(sg, a.tx + t * 3 * n + 2 * n + c);
-        if (a.tp) __builtin_nontemporal_store(lp, a.tp + t * n + c);
+        if (a.tx) __builtin_nontemporal_store(f.sg, a.tx + t * 3 * n + 2 * n + c);
+        if (a.tp) __builtin_nontemporal_store(f.lp, a.tp + t * n + c);
       }
     }
   }
   if (live) {
     if (!hi) {
-      a.state[c] = b0;
-      a.state[n + c] = b1;
+      a.state[c] = f.b0;
+      a.state[n + c] = f.b1;
     } else {
-      a.state[2 * n + c] = sg;
-      a.lp_state[c] = lp;
+      a.state[2 * n + c] = f.sg;
+      a.lp_state[c] = f.lp;
     }
   }
 }
@@ -388,7 +500,7 @@ hipError_t launch_linreg_gibbs(const LinregArgs &h, hipStream_t s) {
     const dim3 grid2((unsigned)((2 * h.n + kBlock - 1) / kBlock));
     hipLaunchKernelGGL(linreg_pair_kernel, grid2, block, 0, s, a);
   } else if (h.mode == PBH_RNG_PHILOX) {
-    hipLaunchKernelGGL(linreg_gibbs_kernel<false>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(linreg_fast_kernel, grid, block, 0, s, a);
   } else {
     const size_t lds = (size_t)(2 * h.n_obs) * sizeof(double);
     if (lds > 65536) {
