@@ -565,6 +565,9 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   if (check_ptr(e, "engine") || check_ptr(init, "init")) return PBH_ERR_ARG;
   if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
   if (n < 1 || off < 0) return fail(PBH_ERR_ARG, "bad n_chains/offset");
+  // kernels address a chain's trace word through a 32-bit buffer offset
+  // (chain * 8 bytes; per-GPU shards of 2^28 chains are far above the 288 GB)
+  if (n > ((int64_t)1 << 28)) return fail(PBH_ERR_ARG, "n_chains > 2^28 per engine");
   const int d = e->d;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));

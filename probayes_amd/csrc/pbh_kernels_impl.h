@@ -2355,7 +2355,8 @@ inline bool pair_form(const KArgs &a) {
 inline bool gmm_pair_form(const KArgs &a) {
   return a.rng == PBH_RNG_PHILOX && a.simple_acc && a.pair_ok && a.ufun == 0 &&
          a.vint == 0 && a.bnd_on == 0 && !a.has_prior && !a.debug && !a.has_tfun &&
-         a.d * a.n * 8 < (int64_t(1) << 32);   // 32-bit trace byte offsets
+         (a.d > 4 ? a.d : 4) * a.n * 8 < (int64_t(1) << 32);   // 32-bit trace byte
+                                                               // offsets (quad: 4 rows)
 }
 
 // The quad kernel's steady-state form applies (see mh_gmm_quad_kernel FULL):
