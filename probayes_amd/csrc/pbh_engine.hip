@@ -41,6 +41,7 @@ struct pbh_engine {
   uint64_t seed = 0;
   double *rep = nullptr;
   int64_t rep_steps = 0, rep_g0 = 0;
+  size_t rep_alloc = 0;          // doubles allocated at rep (device streams reuse it)
   uint32_t *xo = nullptr;      // xoshiro128** states [4][2][n]
   bool xo_seeded = false;
   // legacy NumPy RandomState per chain (pbh_legacy_seed)
@@ -605,6 +606,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   e->mom_steps = 0;
   e->rec_base = 0;
   dfree(e->rep);
+  e->rep_alloc = 0;
   e->rep_steps = 0;
   e->rep_g0 = 0;
   return PBH_OK;
@@ -651,6 +653,7 @@ int pbh_upload_replay(pbh_engine *e, int64_t n_steps, const double *rand) {
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   rc = dalloc(e->rep, (size_t)n_steps * R * n);
+  e->rep_alloc = rc ? 0 : (size_t)n_steps * R * n;
   if (rc) return rc;
   // Reorder draws so that device row k feeds dim k (GAUSS Delta keyword
   // order); the threshold row (index d for MH) stays last.
@@ -706,7 +709,14 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   const int64_t n = e->n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  rc = dalloc(e->rep, (size_t)n_steps * R * n);
+  // consecutive stream generations of the same (or a smaller) size reuse the
+  // buffer: a 250-step cfg2-width stream is 1.4 GB, and a free + malloc of it
+  // per call was 0.3-0.5 ms of the call
+  const size_t need = (size_t)n_steps * R * n;
+  if (!e->rep || e->rep_alloc < need) {
+    rc = dalloc(e->rep, need);
+    e->rep_alloc = rc ? 0 : need;
+  }
   if (!rc && !e->has_gibbs) {
     rc = dalloc(e->mt_order, e->d);
     if (!rc) HIP_TRY(hipMemcpy(e->mt_order, e->draw_order.data(),

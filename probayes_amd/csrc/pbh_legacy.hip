@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *po
 
 struct Mt {
   static constexpr bool kLockstep = false;
+  static constexpr bool kPeek = false;
   uint32_t *key;
   int64_t n, c;
   int pos;
@@ -140,6 +141,7 @@ __device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b) {
 
 struct Mt2 {
   static constexpr bool kLockstep = true;
+  static constexpr bool kPeek = false;
   static constexpr int kRefill = 312;
   uint4 *key;
   int64_t n, c;
@@ -350,6 +352,7 @@ __device__ __attribute__((noinline)) int mt3_refill_cold(w4 *key, int64_t n, int
 template <int H>
 struct Mt3 {
   static constexpr bool kLockstep = true;
+  static constexpr bool kPeek = true;   // attempts2 / advance
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;   // window quads per lane (a power of two)
   static constexpr int kTB = 14;     // twist batch (56 = 4 x 14, 98 = 7 x 14)
@@ -481,6 +484,47 @@ struct Mt3 {
     }
     const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
     return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+
+  // Two polar attempts read ahead without consuming: the four doubles
+  // (x1, x2 of attempt a, x1, x2 of attempt b) at words pos .. pos + 7
+  // (pos even: two quads, or three when pos is 2 mod 4), as 2 d - 1.
+  __device__ __forceinline__ void attempts2(double &x1a, double &x2a, double &x1b,
+                                            double &x2b) {
+    if (pos == kN) {
+      buf ^= 1;
+      pos = 0;
+      pend = 1;
+      ++blk;
+    }
+    const int k = aq();
+    if (k + 2 >= hq) refill_cold();   // fewer than 3 quads staged (rare)
+    const w4 A = slot(k), B = slot(k + 1), C = slot(k + 2);
+    const bool lo = (pos & 3) == 0;
+    const uint32_t w0 = temper(lo ? A.x : A.z), w1 = temper(lo ? A.y : A.w);
+    const uint32_t w2 = temper(lo ? A.z : B.x), w3 = temper(lo ? A.w : B.y);
+    const uint32_t w4_ = temper(lo ? B.x : B.z), w5 = temper(lo ? B.y : B.w);
+    const uint32_t w6 = temper(lo ? B.z : C.x), w7 = temper(lo ? B.w : C.y);
+    auto dbl = [](uint32_t a, uint32_t b) {
+      const int32_t ai = (int32_t)(a >> 5), bi = (int32_t)(b >> 6);
+      return (ai * 67108864.0 + bi) / 9007199254740992.0;
+    };
+    x1a = 2.0 * dbl(w0, w1) - 1.0;
+    x2a = 2.0 * dbl(w2, w3) - 1.0;
+    x1b = 2.0 * dbl(w4_, w5) - 1.0;
+    x2b = 2.0 * dbl(w6, w7) - 1.0;
+  }
+
+  // consume nw (4 or 8) words read by attempts2
+  __device__ __forceinline__ void advance(int nw) {
+    pos += nw;
+    if (pos > kN) {   // (pos == kN flips lazily, as in next_double)
+      pos -= kN;
+      buf ^= 1;
+      pend = 1;
+      ++blk;
+    }
+    if (pos & 3) cur = slot(aq());
   }
 
   __device__ __forceinline__ int packed() const {
@@ -617,14 +661,41 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       }
       const int need = (a.d - j0 + 1) / 2;   // pairs this lane draws
       int np = 0;
-      while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
-        if (np < need) {
-          const double x1 = 2.0 * m.next_double() - 1.0;
-          const double x2 = 2.0 * m.next_double() - 1.0;
-          const double r2 = x1 * x1 + x2 * x2;
-          if (r2 < 1.0 && r2 != 0.0) {
-            stage[np * blockDim.x + threadIdx.x] = make_double2(x1, x2);
-            ++np;
+      if constexpr (M::kPeek) {
+        // two attempts per lockstep iteration (read ahead from the window,
+        // consumed only as far as they are used): ~5.5 iterations for 5
+        // pairs instead of ~9.5, and two independent chains of arithmetic
+        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+          if (np < need) {
+            double x1a, x2a, x1b, x2b;
+            m.attempts2(x1a, x2a, x1b, x2b);
+            const double r2a = x1a * x1a + x2a * x2a;
+            const double r2b = x1b * x1b + x2b * x2b;
+            if (r2a < 1.0 && r2a != 0.0) {
+              stage[np * blockDim.x + threadIdx.x] = make_double2(x1a, x2a);
+              ++np;
+            }
+            int used = 4;
+            if (np < need) {
+              used = 8;
+              if (r2b < 1.0 && r2b != 0.0) {
+                stage[np * blockDim.x + threadIdx.x] = make_double2(x1b, x2b);
+                ++np;
+              }
+            }
+            m.advance(used);
+          }
+        }
+      } else {
+        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+          if (np < need) {
+            const double x1 = 2.0 * m.next_double() - 1.0;
+            const double x2 = 2.0 * m.next_double() - 1.0;
+            const double r2 = x1 * x1 + x2 * x2;
+            if (r2 < 1.0 && r2 != 0.0) {
+              stage[np * blockDim.x + threadIdx.x] = make_double2(x1, x2);
+              ++np;
+            }
           }
         }
       }
