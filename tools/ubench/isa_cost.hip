@@ -170,6 +170,48 @@ __global__ void k_cnd_salu_sgpr(uint32_t *out, uint32_t s) {
   for (int j = 0; j < 8; ++j) x ^= v[j];
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
+// other VOP2 forms with an implicit VCC operand: carry-in add (64-bit address
+// arithmetic), against its VOP3 form with an SGPR-pair carry
+__global__ void k_addc_e32(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a), "v"(s) : "vcc");
+  for (int i = 0; i < R; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_addc_co_u32_e32 %0, vcc, %0, %1, vcc" : "+v"(v[j]) : "v"(a) : "vcc");
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ void k_addc_e64(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  for (int i = 0; i < R; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_addc_co_u32_e64 %0, s[40:41], %0, %1, s[42:43]" : "+v"(v[j]) : "v"(a) : "s40", "s41");
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+__global__ void k_add_co_e32(uint32_t *out, uint32_t s) {
+  uint32_t v[8];
+  const uint32_t a = threadIdx.x * 7 + s;
+  for (int j = 0; j < 8; ++j) v[j] = a + j;
+  for (int i = 0; i < R; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(v[j]) : "v"(a) : "vcc");
+  }
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j) x ^= v[j];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
 // cmp + cndmask pair as the compiler emits a select (v_cmp -> s[..] -> cndmask)
 __global__ void k_sel(uint32_t *out, uint32_t s) {
   uint32_t v[8];
@@ -241,6 +283,8 @@ int main(int argc, char **argv) {
       {"v_cndmask_e32(vcc)", k_cnd_vcc}, {"select(cmp+cnd)/2", k_sel},
       {"v_cndmask_e64(vcc)", k_cnd_e64_vcc}, {"s_mov vcc+8 e32(vcc)", k_cnd_salu_vcc},
       {"s_mov sgpr+8 e64(sgpr)", k_cnd_salu_sgpr},
+      {"v_addc_co_u32_e32(vcc)", k_addc_e32}, {"v_addc_co_u32_e64(sgpr)", k_addc_e64},
+      {"v_add_co_u32_e32(vcc)", k_add_co_e32},
       {"LAT v_fma_f64", k_fma64_lat}, {"LAT v_xor_b32", k_xor_lat},
       {"LAT v_mad_u64_u32", k_mad64_lat}};
   printf("%-24s %8s %8s %8s %8s\n", "instruction", "1w/SIMD", "2w/SIMD",
