@@ -389,6 +389,21 @@ __device__ __forceinline__ float sel_f32(uint64_t m, float if0, float if1) {
                                            __builtin_bit_cast(uint32_t, if1)));
 }
 
+// 1/x and 1/sqrt(x) for positive normal x: the hardware v_rcp_f64 /
+// v_rsq_f64 estimate and two Newton steps (within an ulp or two of the IEEE
+// forms), for the production (non-replay) arithmetic.
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+  return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * __builtin_fma(-hx * y, y, 1.5);
+  return y * __builtin_fma(-hx * y, y, 1.5);
+}
+
 // 16-bit store through a buffer resource (accept words of the 16-chain
 // kernels); base wave-uniform as in st_buf.
 __device__ __forceinline__ void st_buf16(void *base, uint32_t voff, uint16_t v) {

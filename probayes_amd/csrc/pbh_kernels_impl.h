@@ -597,13 +597,14 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
           sq[k] = dl[k] * dl[k];
         }
         const double ss = np_sum_regs<D>(sq, D);
-        const double rss = ss >= kNearlyPosZero ? sqrt(ss) : 0.;
         if (FAST) {
-          // production: one division for the radius scale
-          const double sc = d0 / rss;
+          // production: the radius scale d0 / sqrt(ss) from one inverse
+          // square root (no IEEE sqrt and division on the step's chain)
+          const double sc = ss >= kNearlyPosZero ? d0 * rsq_nr(ss) : __builtin_inf();
 #pragma unroll
           for (int k = 0; k < D; ++k) dl[k] = (dl[k] * sc) * cld(a.plen, k);
         } else {
+          const double rss = ss >= kNearlyPosZero ? sqrt(ss) : 0.;
 #pragma unroll
           for (int k = 0; k < D; ++k) dl[k] = ((dl[k] * d0) / rss) * cld(a.plen, k);
         }

@@ -237,17 +237,6 @@ linreg_gibbs_kernel(LinregK a) {
 //   v.prob:  -ss yp / 2 - n (logC + log sg),  yp = 1/sg^2.
 // yp and log sg are pure functions of sg (cached between y_sigma steps and
 // recomputed at launch entry), so launch splits give identical chains.
-__device__ __forceinline__ double rcp_nr(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  r = __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
-  return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
-}
-__device__ __forceinline__ double rsq_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  const double hx = 0.5 * x;
-  y = y * __builtin_fma(-hx * y, y, 1.5);
-  return y * __builtin_fma(-hx * y, y, 1.5);
-}
 
 struct FastState {
   double b0, b1, sg, yp, lsg, lp;
