@@ -295,28 +295,47 @@ __device__ __attribute__((noinline)) double mt_gamma_tail(const LinregK &a, cons
 // whose first Marsaglia-Tsang attempt (blocks (cycle, 1), (cycle, 1 + 2^16))
 // is computed beside the normals (three independent Philox blocks, two
 // Box-Muller pairs); a rejected first attempt continues out of line.
-__device__ __forceinline__ void cycle_draws(const LinregK &a, const BMTables *tb,
-                                            int64_t gc, int64_t cycle, double cm,
-                                            double dg, double &z0, double &z1,
-                                            double &g) {
+// A cycle's draws in two parts.  cycle_head: the beta normals (block
+// (cycle, 0)) and the y_sigma gamma's first Marsaglia-Tsang proposal (blocks
+// (cycle, 1), (cycle, 1 + 2^16)) -- three independent Philox blocks and two
+// Box-Muller pairs, branch-free.  cycle_gamma: the attempt's squeeze / log
+// tests and, when it is rejected, the remaining attempts out of line.
+struct CycleHead {
+  double z0, z1, t, v, u, z2;
+};
+
+__device__ __forceinline__ CycleHead cycle_head(const LinregK &a, const BMTables *tb,
+                                                int64_t gc, int64_t cycle, double cm) {
   const u32x4 wn = draw_block(a, gc, cycle, 0u);
   const u32x4 wg = draw_block(a, gc, cycle, 1u);
   const u32x4 wu = draw_block(a, gc, cycle, 1u + 0x10000u);
+  CycleHead h;
   double zg, zg1;
-  normal_pair<false>(wn, tb, z0, z1);
+  normal_pair<false>(wn, tb, h.z0, h.z1);
   normal_pair<false>(wg, tb, zg, zg1);
-  const double t = 1.0 + cm * zg;
-  const double v = t * t * t;
-  const double u = 1.0 - u01(wu.x, wu.y);
-  const double z2 = zg * zg;
-  bool done = t > 0.0 && u < 1.0 - 0.0331 * (z2 * z2);
-  if (!done && t > 0.0) done = fast_log(u) < 0.5 * z2 + dg - dg * v + dg * fast_log(v);
-  g = dg * v;
-  if (!done) g = mt_gamma_tail(a, tb, gc, cycle, t > 0.0 ? dg * v : dg);
+  h.t = 1.0 + cm * zg;
+  h.v = h.t * h.t * h.t;
+  h.u = 1.0 - u01(wu.x, wu.y);
+  h.z2 = zg * zg;
+  return h;
 }
 
-// PHILOX production kernel, one chain per lane: the draws of each 3-step
-// cycle come first (cycle_draws), then the cycle's O(1) updates (fast_step).
+__device__ __forceinline__ double cycle_gamma(const LinregK &a, const BMTables *tb,
+                                              int64_t gc, int64_t cycle, double dg,
+                                              const CycleHead &h) {
+  bool done = h.t > 0.0 && h.u < 1.0 - 0.0331 * (h.z2 * h.z2);
+  if (!done && h.t > 0.0)
+    done = fast_log(h.u) < 0.5 * h.z2 + dg - dg * h.v + dg * fast_log(h.v);
+  double g = dg * h.v;
+  if (!done) g = mt_gamma_tail(a, tb, gc, cycle, h.t > 0.0 ? dg * h.v : dg);
+  return g;
+}
+
+// PHILOX production kernel, one chain per lane, software-pipelined by cycle:
+// while a 3-step cycle's O(1) updates run (a dependent chain), the NEXT
+// cycle's Philox blocks and Box-Muller pairs are computed beside them in the
+// same basic block; its gamma tests follow the updates.  Partial cycles at a
+// launch's ends take the same draws one step at a time.
 __global__ void __launch_bounds__(kBlock)
 linreg_fast_kernel(LinregK a) {
   __shared__ BMTables s_bmt;
@@ -333,12 +352,7 @@ linreg_fast_kernel(LinregK a) {
   const double nd = (double)a.n_obs;
   const double dg = a.alpha - 1.0 / 3.0;
   const double cm = 1.0 / sqrt(9.0 * dg);
-  double z0 = 0., z1 = 0., g = 0.;
-  for (int64_t t = 0; t < a.n_steps; ++t) {
-    const int64_t step = a.step0 + t;
-    const int key = (int)(step % 3);
-    if (key == 0 || t == 0) cycle_draws(a, &s_bmt, gc, step / 3, cm, dg, z0, z1, g);
-    fast_step(a, key, key == 0 ? z0 : (key == 1 ? z1 : g), nd, f);
+  auto record = [&](int64_t t) {
     if (a.tx) {
       double *tx = a.tx + t * 3 * n;
       __builtin_nontemporal_store(f.b0, tx + c);
@@ -346,6 +360,36 @@ linreg_fast_kernel(LinregK a) {
       __builtin_nontemporal_store(f.sg, tx + 2 * n + c);
     }
     if (a.tp) __builtin_nontemporal_store(f.lp, a.tp + t * n + c);
+  };
+  int64_t t = 0;
+  int64_t cycle = a.step0 / 3;
+  CycleHead h = cycle_head(a, &s_bmt, gc, cycle, cm);
+  double g = cycle_gamma(a, &s_bmt, gc, cycle, dg, h);
+  // a launch starting inside a cycle: its remaining steps
+  for (int key = (int)(a.step0 % 3); key != 0 && key < 3 && t < a.n_steps; ++key, ++t) {
+    fast_step(a, key, key == 1 ? h.z1 : g, nd, f);
+    record(t);
+  }
+  if (a.step0 % 3 != 0 && t < a.n_steps) {   // on to the next whole cycle
+    ++cycle;
+    h = cycle_head(a, &s_bmt, gc, cycle, cm);
+    g = cycle_gamma(a, &s_bmt, gc, cycle, dg, h);
+  }
+  for (; t + 3 <= a.n_steps; t += 3) {
+    const CycleHead hn = cycle_head(a, &s_bmt, gc, cycle + 1, cm);
+    fast_step(a, 0, h.z0, nd, f);
+    record(t);
+    fast_step(a, 1, h.z1, nd, f);
+    record(t + 1);
+    fast_step(a, 2, g, nd, f);
+    record(t + 2);
+    ++cycle;
+    h = hn;
+    g = cycle_gamma(a, &s_bmt, gc, cycle, dg, h);
+  }
+  for (int key = 0; t < a.n_steps; ++key, ++t) {   // a trailing partial cycle
+    fast_step(a, key, key == 0 ? h.z0 : h.z1, nd, f);
+    record(t);
   }
   a.state[c] = f.b0;
   a.state[n + c] = f.b1;
