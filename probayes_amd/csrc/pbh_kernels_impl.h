@@ -1997,6 +1997,7 @@ struct GibbsFast {
   double zlo[M], zhi[M];   // truncation limits of the owned coordinates' z
   double xo[M];     // owned dims of x (the state)
   double zo[M];     // this cycle's normals of the owned coordinates
+  double zn[M];     // the next cycle's, drawn during this one (full cycles)
   double go[M];     // owned dims of g = P'(x - mu')
   double ms[M], mq[M];   // running moments of the owned dims
   double Q;         // (x - mu')^T g (identical in the group)
@@ -2049,16 +2050,27 @@ struct GibbsFast {
   // cycle starting at step gc, from Philox blocks 0x100 + 16 p + b.
   const BMTables *bmt;   // LDS tables of the normals' log and sin / cos
 
-  __device__ __forceinline__ void draw_cycle(const KArgs &a, int64_t gc,
-                                             int64_t chain) {
+  // the cycle's Box-Muller normals (branch-free)
+  __device__ __forceinline__ void draw_raw(const KArgs &a, int64_t gc, int64_t chain,
+                                           double (&z)[M]) {
 #pragma unroll
     for (int b = 0; b < (M + 1) / 2; ++b) {
       double z0, z1;
       box_muller_tab(philox4x32_10(ctr(0x100u + 16u * p + b, gc, chain),
                                    a.seed_lo, a.seed_hi), bmt, z0, z1);
-      zo[2 * b] = z0;
-      if (2 * b + 1 < M) zo[2 * b + 1] = z1;
+      z[2 * b] = z0;
+      if (2 * b + 1 < M) z[2 * b + 1] = z1;
     }
+  }
+
+  __device__ __forceinline__ void draw_cycle(const KArgs &a, int64_t gc,
+                                             int64_t chain) {
+    draw_raw(a, gc, chain, zo);
+    fix_trunc(a, gc, chain);
+  }
+
+  __device__ __forceinline__ void fix_trunc(const KArgs &a, int64_t gc,
+                                            int64_t chain) {
     // Truncation (cond_cov.py:57-62): a normal outside coordinate k's limits
     // is replaced by the reference's inversion draw ppf(U(cdf_lo, cdf_hi)).
     // Rare; one wave-uniform loop keeps a single copy of ndtri in the code.
@@ -2263,18 +2275,32 @@ void gibbs_fast_kernel(KArgs a) {
   __builtin_amdgcn_s_waitcnt(0);
   int s = 0;
   bool entry = true;   // the entry drew the current cycle already
+  bool have_next = false;   // zn holds this cycle's normals (wave-uniform)
   while (s < a.n_steps) {
     if (cm == 0) {     // a coordinate cycle starts
-      if (!entry) st.draw_cycle(a, a.g0 + s, chain);
+      if (!entry) {
+        if (have_next) {
+#pragma unroll
+          for (int ii = 0; ii < M; ++ii) st.zo[ii] = st.zn[ii];
+          st.fix_trunc(a, a.g0 + s, chain);
+        } else {
+          st.draw_cycle(a, a.g0 + s, chain);
+        }
+      }
       if ((cyc & (kRefreshCycles - 1)) == 0) st.refresh(a);
       ++cyc;
     }
     entry = false;
+    have_next = false;
     const int nst = min(nblk - cm / ts, a.n_steps - s);   // steps in this cycle
     const int ke = min(D, cm + nst * ts);
-    if (ts == 1 && cm == 0 && ke == D)
+    if (ts == 1 && cm == 0 && ke == D) {
+      // software pipelining: the next cycle's Philox blocks and Box-Muller
+      // pairs (state-independent) beside this cycle's dependent updates
+      st.draw_raw(a, a.g0 + s + D, chain, st.zn);
+      have_next = true;
       st.template cycle<true>(a, 0, D, post_mask, std::make_integer_sequence<int, D>{});
-    else
+    } else
       st.template cycle<false>(a, cm, ke, post_mask, std::make_integer_sequence<int, D>{});
     s += nst;
     cm = ke == D ? 0 : ke;
