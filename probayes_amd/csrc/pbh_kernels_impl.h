@@ -1500,15 +1500,25 @@ __device__ __forceinline__ Decision accept_filter_ms32(double Mp, float Sp,
 // 7.1e-7 + 1 ulp per term, the sum within 1.1e-6, rcp and the conversion of S
 // 1.8e-7: about 1.4e-6 < 4e-6.  e = inf (a far better proposal) accepts;
 // e = 0 with lead 0 is undecided.  inr: |M'|, |lm| <= 698 as before.
+// Form used by the quad kernel: the state's fp32 sum ls32 scales the
+// threshold instead of dividing the proposal's sum (e = sp / ls32, t < e
+// <=> t ls32 < sp; ls32 > 0): no reciprocal per step; the two products add
+// an ulp each, inside the same 4e-6 margin.
 template <int LB>
-__device__ __forceinline__ Decision accept_filter_rel32(float e, bool inr,
+__device__ __forceinline__ Decision accept_filter_rel32(float sp, float ls32, bool inr,
                                                         uint32_t lead) {
   constexpr float w = 1.0f / (float)(1u << LB);
   const float tlo = (float)lead * w;
   const float thi = tlo + w;
-  const bool af = thi <= e * 0.999996f;
-  const bool rf = tlo > e * 1.000004f;
+  const bool af = thi * ls32 <= sp * 0.999996f;
+  const bool rf = tlo * ls32 > sp * 1.000004f;
   return Decision{(bool)(inr & af), !(inr & (af | rf))};
+}
+
+__device__ __forceinline__ double max_f64_raw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 template <int CTRL>
@@ -1571,7 +1581,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   for (int i = 0; i < D; ++i) x[i] = a.x[i * a.n + cc];
   const double lp0 = a.lp[cc];
   double lm = lp0, ls = 1.0;   // the state's density as (M, S): lp = M + ln S
-  float lr32 = 1.0f;           // 1 / fp32(S) of the state (the decision path)
+  float ls32 = 1.0f;           // fp32(S) of the state (the decision path)
   int64_t nacc = 0;
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
@@ -1625,10 +1635,12 @@ void mh_gmm_quad_kernel(KArgs a) {
       // 0 to within 2^-1074)
       float e32 = __builtin_amdgcn_exp2f((float)((v - lm) * 1.4426950408889634));
       e32 = e32 + qperm_f32<kQuadXor1>(e32);
-      const float E32 = (e32 + qperm_f32<kQuadXor2>(e32)) * lr32;
+      const float E32 = e32 + qperm_f32<kQuadXor2>(e32);   // the proposal's sum
       // record path (off the decision's chain): M' and S in fp64
-      double M = __builtin_fmax(v, qperm_f64<kQuadXor1>(v));
-      M = __builtin_fmax(M, qperm_f64<kQuadXor2>(M));
+      // v_max_f64 without the compiler's canonicalising max of the DPP'd
+      // operand (the values are never NaN: finite or -inf)
+      double M = max_f64_raw(v, qperm_f64<kQuadXor1>(v));
+      M = max_f64_raw(M, qperm_f64<kQuadXor2>(M));
       const double dv = v - M;
       const bool inr = (__builtin_fabs(M) <= 698.) & (__builtin_fabs(lm) <= 698.);
       double e = exp_tab(dv, s_bmt);
@@ -1636,7 +1648,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
       bool acc;
       if constexpr (FULL) {
-        const Decision dc = accept_filter_rel32<LB>(E32, inr, lead);
+        const Decision dc = accept_filter_rel32<LB>(E32, ls32, inr, lead);
         acc = dc.acc;
         if (__ballot(dc.need)) {   // wave-uniform, rare
           if (dc.need) acc = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
@@ -1645,7 +1657,7 @@ void mh_gmm_quad_kernel(KArgs a) {
         acc = true;                                  // s = None on step 1
       } else {
         const Decision dc = a.acc_beta == 1.0
-            ? accept_filter_rel32<LB>(E32, inr, lead)
+            ? accept_filter_rel32<LB>(E32, ls32, inr, lead)
             : accept_filter_lead<LB>((M + ln_tab(S, s_bmt)) * a.acc_beta,
                                      (lm + ln_tab(ls, s_bmt)) * a.acc_beta,
                                      lead, false);
@@ -1664,7 +1676,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
       lm = acc ? M : lm;
       ls = acc ? S : ls;
-      lr32 = acc ? __builtin_amdgcn_rcpf((float)S) : lr32;
+      ls32 = acc ? (float)S : ls32;
       gm[j] = lm;
       gs[j] = ls;
       if constexpr (MOM) {
