@@ -203,14 +203,36 @@ int pbh_set_rng(pbh_engine *eng, int32_t mode, uint64_t seed);
  * (Philox counter, CondCov cycle phase), whether step 1 is behind (the
  * auto-accept, sp.py:231-232), and for XOSHIRO the per-chain generator
  * state [8][N] (NULL otherwise).  pbh_restore goes after pbh_init_chains
- * (same N) and pbh_set_rng, before pbh_alloc_trace; a run from the restored
- * engine continues the checkpointed one step for step.  The production Gibbs
+ * (same N) and pbh_set_rng; it detaches a trace buffer and replay rows
+ * (pbh_alloc_trace again); a run from the restored engine continues the
+ * checkpointed one step for step.  The production Gibbs
  * kernel's persisted g, Q are recomputed from x (v.prob then agrees to its
  * refresh tolerance, 1e-9).                                                 */
 int pbh_get_checkpoint(pbh_engine *eng, double *x, double *lp, int64_t *step,
                        int32_t *has_pred, uint32_t *xo);
 int pbh_restore(pbh_engine *eng, const double *x, const double *lp,
                 int64_t step, int32_t has_pred, const uint32_t *xo);
+/* The device legacy streams' state for a checkpoint (pbh_legacy_seed):
+ * key [words][N] with words = 624 per chain (1248 double-buffered,
+ * pbh_legacy_state_words), the read position pos [N], the cached-gauss flag
+ * has [N] and value gauss [N] (NumPy's RandomState has_gauss / gauss).
+ * After pbh_restore on an engine with legacy streams, pbh_legacy_replay
+ * refuses until pbh_set_legacy_state restores the checkpoint's state.       */
+int pbh_legacy_state_words(pbh_engine *eng, int64_t *words_per_chain);
+int pbh_get_legacy_state(pbh_engine *eng, uint32_t *key, int32_t *pos,
+                         int32_t *has, double *gauss);
+int pbh_set_legacy_state(pbh_engine *eng, const uint32_t *key,
+                         const int32_t *pos, const int32_t *has,
+                         const double *gauss);
+/* Replaces the chains' state (x [N][d], lp [N]), the global step and the
+ * step-1 flag at any point; every generator state (xoshiro, legacy streams)
+ * continues where it is.  The trace buffer and the replay rows are
+ * detached: pbh_alloc_trace / pbh_upload_replay / pbh_legacy_replay again
+ * before pbh_run.  Used by the SP facade's incremental samplers (SP.reset,
+ * sp.py:113-128) to restart chains at init or to rewind to the last step
+ * handed out.                                                               */
+int pbh_set_chains(pbh_engine *eng, const double *x, const double *lp,
+                   int64_t step, int32_t has_pred);
 /* Replay stream [n_steps][R][n_chains] (R = d + 1 for MH, 1 for Gibbs),
  * consumed from the next pbh_run step on.                                   */
 int pbh_upload_replay(pbh_engine *eng, int64_t n_steps, const double *rand);
@@ -358,10 +380,11 @@ int pbh_check_accept(int device, int64_t n, const double *lp,
 int pbh_check_normals(int device, int64_t n, const uint32_t *words,
                       double *fast, double *ref);
 
-/* The production fp64 normals (bm64_pair, PBH_RNG_PHILOX / XOSHIRO) on n
- * blocks words[n][4]: fast[n][2] = bm64_pair, ref[n][2] = the same u1 and
- * angle through libm log / sqrt / sincos.  pbh_bm64_tables fills out[2564]
- * with the engine's tables ({-2 ln(c_j/2), 1/c_j} x 1025, {sin, cos} x 257). */
+/* The production fp64 normals (bm96_pair, PBH_RNG_PHILOX / XOSHIRO) on n
+ * word triples words[n][3]: fast[n][2] = bm96_pair, ref[n][2] = the same u1
+ * and angle through libm log / sqrt / sincos.  pbh_bm64_tables fills
+ * out[4162] with the engine's tables ({-2 ln c_j, 1/c_j} x 1025, {sin, cos}
+ * x 1024 over the full turn, 2^(i/64) x 64).                                */
 int pbh_check_normals64(int device, int64_t n, const uint32_t *words,
                         double *fast, double *ref);
 int pbh_bm64_tables(double *out);

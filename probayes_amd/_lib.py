@@ -31,6 +31,7 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int32)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
+_i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 
@@ -115,6 +116,14 @@ SIGNATURES = {
                                           _u32p]),
     'pbh_restore': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp, ctypes.c_int64,
                                    ctypes.c_int32, _u32p]),
+    'pbh_set_chains': (ctypes.c_int, [ctypes.c_void_p, _dp, _dp, ctypes.c_int64,
+                                      ctypes.c_int32]),
+    'pbh_legacy_state_words': (ctypes.c_int, [ctypes.c_void_p,
+                                              ctypes.POINTER(ctypes.c_int64)]),
+    'pbh_get_legacy_state': (ctypes.c_int, [ctypes.c_void_p, _u32p, _i32p, _i32p,
+                                            _dp]),
+    'pbh_set_legacy_state': (ctypes.c_int, [ctypes.c_void_p, _u32p, _i32p, _i32p,
+                                            _dp]),
     'pbh_trace_expectation': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_double,
                                              _dp]),

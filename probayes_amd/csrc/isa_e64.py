@@ -9,9 +9,18 @@ shrinks to VOP2 when the mask was allocated to VCC.  Forms VOP3 cannot encode
 on gfx9 are left alone: a literal src0, and an SGPR src0 (with VCC it would
 be a second constant-bus read).
 A function is rewritten only if its assembled size plus 4 bytes per
-rewritten select stays below 128 KB: then every branch inside it still fits
+rewritten select (and per added s_nop) stays below 128 KB: then every branch inside it still fits
 the 16-bit dword offset the compiler's branch relaxation assumed (larger
 functions keep their VOP2 selects).
+Hazard: VOP2 reads VCC implicitly, VOP3 as an explicit SGPR source, and a
+VALU write of an SGPR followed by a VALU read of it as an SGPR operand needs
+two wait states on gfx950 -- the compiler's hazard recognizer puts `s_nop 1`
+between a v_cmp_*_e64 writing a mask and the v_cndmask_b32_e64 reading it
+(every such pair in this build), and nothing between a VALU VCC write and
+a VOP2 select.  So a rewritten select whose VCC was written by a VALU
+instruction less than two wait states before it (counting instructions and
+s_nop N as N + 1), or that follows a label within that window (a writer may
+sit in any predecessor block), gets the missing wait states as an s_nop.
 usage: isa_e64.py <in.s> <out.s> [<llvm-readelf -s of the assembled in.s>]"""
 import re
 import sys
@@ -30,6 +39,35 @@ def ok_src0(s):
 
 
 FUNC = re.compile(r'^([A-Za-z_.$][\w.$]*):')
+LABEL = re.compile(r'^\s*([A-Za-z_.$%][\w.$]*):')
+# VALU instructions that write VCC: VOPC e32 compares, carry-out e32 forms,
+# and VOP3 forms with vcc as the scalar destination (second operand)
+VCC_E32 = re.compile(r'^v_(cmpx?_\w+|add_co_u32|sub_co_u32|subrev_co_u32|addc_co_u32|'
+                     r'subb_co_u32|subbrev_co_u32)_e32\b')
+VCC_SDST = re.compile(r'^v_\w+\s+[^,]+,\s*vcc\s*,')
+VCC_VOPC3 = re.compile(r'^v_cmpx?_\w+_e64\s+vcc\s*,')
+
+
+def writes_vcc(ins):
+  return bool(VCC_E32.match(ins) or VCC_SDST.match(ins) or VCC_VOPC3.match(ins))
+
+
+def wait_needed(prev):
+  """Wait states to add before a VOP3 read of VCC, given the instructions
+  before it (nearest last; None marks a label)."""
+  ws = 0
+  for ins in reversed(prev):
+    if ws >= 2:
+      return 0
+    if ins is None:
+      return 2 - ws
+    if ins.startswith('s_nop'):
+      ws += int(ins.split()[1], 0) + 1
+      continue
+    if ins.startswith('v_') and writes_vcc(ins):
+      return 2 - ws
+    ws += 1
+  return 0
 LIMIT = 128 * 1024 - 256
 
 
@@ -45,39 +83,58 @@ def sizes(path):
   return out
 
 
+def rewrite(lines, owner, allowed):
+  """The rewritten lines, (selects rewritten, s_nops added, selects kept) and
+  the bytes each function grows by."""
+  n = kept = nops = 0
+  out, grow = [], {}
+  prev = []   # the last few instructions (None for a label)
+  for line, func in zip(lines, owner):
+    m = PAT.match(line.rstrip('\n'))
+    if m and ok_src0(m.group(4)) and func in allowed:
+      w = wait_needed(prev)
+      if w:
+        out.append('{}s_nop {}\n'.format(m.group(1), w - 1))
+        prev.append('s_nop {}'.format(w - 1))
+        nops += 1
+        grow[func] = grow.get(func, 0) + 4
+      line = '{}v_cndmask_b32_e64{}{}, {}, {}, vcc\n'.format(
+          m.group(1), m.group(2), m.group(3), m.group(4).strip(), m.group(5))
+      grow[func] = grow.get(func, 0) + 4
+      n += 1
+    elif 'v_cndmask_b32_e32' in line:
+      kept += 1
+    out.append(line)
+    t = line.split(';')[0].strip()
+    if LABEL.match(line) and not t.startswith('.set'):
+      prev.append(None)
+    elif t and not t.startswith('.'):
+      prev.append(t)
+    prev = prev[-4:]
+  return out, (n, nops, kept), grow
+
+
 def main():
   src, dst = sys.argv[1], sys.argv[2]
   size = sizes(sys.argv[3] if len(sys.argv) > 3 else None)
   lines = open(src).readlines()
-  # per function: the number of convertible selects, to decide whether the
-  # grown function still keeps every branch within range
-  func, grow, owner = None, {}, []
+  func, owner = None, []
   for line in lines:
     fm = FUNC.match(line)
     if fm and not fm.group(1).startswith('.L'):
       func = fm.group(1)
-    m = PAT.match(line.rstrip('\n'))
-    if m and ok_src0(m.group(4)) and func is not None:
-      grow[func] = grow.get(func, 0) + 4
     owner.append(func)
+  # the growth of every function if rewritten, then only those that stay in
+  # the branch range
+  _, _, grow = rewrite(lines, owner, set(owner) - {None})
   allowed = {f for f, g in grow.items() if f in size and size[f] + g < LIMIT}
-  n = kept = 0
-  out = []
-  for line, func in zip(lines, owner):
-    if True:
-      m = PAT.match(line.rstrip('\n'))
-      if m and ok_src0(m.group(4)) and func in allowed:
-        line = '{}v_cndmask_b32_e64{}{}, {}, {}, vcc\n'.format(
-            m.group(1), m.group(2), m.group(3), m.group(4).strip(), m.group(5))
-        n += 1
-      elif 'v_cndmask_b32_e32' in line:
-        kept += 1
-      out.append(line)
+  out, (n, nops, kept), _ = rewrite(lines, owner, allowed)
   with open(dst, 'w') as f:
     f.writelines(out)
   big = sorted(set(grow) - allowed)
-  sys.stderr.write('isa_e64: {} VOP2 selects -> VOP3, {} kept ({}; {} functions '
-                   'too large to rewrite)\n'.format(n, kept, src, len(big)))
+  sys.stderr.write('isa_e64: {} VOP2 selects -> VOP3 ({} behind an s_nop), {} kept '
+                   '({}; {} functions too large to rewrite)\n'.format(
+                       n, nops, kept, src, len(big)))
 
 
 if __name__ == '__main__':

@@ -220,31 +220,39 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 
 // ---------------------------------------------------------------------------
 // Production fp64 normals (PBH_RNG_PHILOX, PBH_RNG_XOSHIRO): Box-Muller on
-// two 52-bit uniforms per pair (the reference draws fp64 normals: NumPy's
-// legacy polar gauss on 53-bit uniforms behind scipy norm.rvs,
-// examples/mcmc/mcmc_prob2.py:31).  One 128-bit block (x, y, z, w) gives
-//   u1 = (k1 + 1/2) 2^-52 in (0, 1), k1 = x[19:0]:y   (never 0 or 1),
-//   alpha = (j + k2 2^-52) (pi/2) / 256,  j = z[29:22], k2 = z[19:0]:w,
-//   z0 = s0 r cos(alpha), z1 = s1 r sin(alpha), r = sqrt(-2 ln u1),
-// with the independent sign bits s0 = z[31], s1 = z[30]: reflecting a
-// uniform quarter-turn angle by two fair signs is the uniform full-turn angle
-// exactly.  Spare bits: x[31:20] (12) and z[21:20] (2).
-//   E = -2 ln u1 = (e + 1)(-2 ln 2) - 2 ln(c_j / 2) + r q(r),  c_j = m rounded
-//             to 10 mantissa bits (j in [0, 1024]), r = (m - c_j) / c_j with
-//             one rounding (m - c_j is exact), |r| <= 2^-11, q(r) =
-//             -2 log1p(r) / r to degree 4 (truncation r^5 / 6 < 2^-58
-//             relative); u1 -> 1 takes c = 2 and ln(c/2) = 0, so E keeps its
-//             relative accuracy there;
+// 96 random bits per pair (the reference draws fp64 normals: NumPy's legacy
+// polar gauss on 53-bit uniforms behind scipy norm.rvs,
+// examples/mcmc/mcmc_prob2.py:31).  Three 32-bit words (a, b, c) give
+//   u1 = (k1 + 1/2) 2^-52 in (0, 1), k1 = b[31:12]:a    (never 0 or 1;
+//        the largest radius is sqrt(2 ln 2^53) = 8.57),
+//   alpha = (J + c 2^-32) 2 pi / 1024,  J = b[11:2]      (a full turn, 42
+//        bits of angle; b[1:0] unused),
+//   z0 = r cos(alpha), z1 = r sin(alpha), r = sqrt(-2 ln u1).
+//   E = -2 ln u1 = e (-2 ln 2) + T_j + r q(r): u1 = m 2^e with m in [1/2, 1)
+//             (v_frexp_mant / v_frexp_exp), c_j = m rounded to 10 fraction
+//             bits (c_j = (1024 + j) / 2048, j in [0, 1024]), T_j = -2 ln c_j,
+//             r = (m - c_j) / c_j with one rounding (m - c_j is exact),
+//             |r| <= 2^-11, q(r) = -2 log1p(r) / r to degree 4 (truncation
+//             r^5 / 6 < 2^-58 relative); u1 -> 1 takes c = 1 and T = 0, so E
+//             keeps its relative accuracy there;
 //   sqrt    = v_rsq_f64 + two Newton steps;
-//   (sin, cos)(alpha) = table angle j rotated by theta < pi/512: sin degree
+//   (sin, cos)(alpha) = table angle J rotated by theta < pi/512: sin degree
 //             5, cos degree 4 (truncations 2e-19 relative, 1e-18 absolute).
+// The bit positions make every index one VALU op: the hi word of 1 + k1
+// 2^-52 is v_alignbit(0x3FF, b, 12), the sin/cos row's byte offset 4 J is
+// b & 0xFFC (the table is four arrays of 32-bit words: sin lo, sin hi, cos
+// lo, cos hi), the log row's byte offset is a v_bfe of c_j's hi word.
 // Tables (host-computed in long double, pbh_dispatch.cpp bm64_tables) live
-// in LDS: 1025 {-2 ln(c_j/2), 1/c_j} pairs and 257 {sin, cos} pairs, 20.5 KB.
-// About 45 VALU per pair.  Accuracy: tests/test_gpu_normals.py (libm form).
+// in LDS: 1025 {-2 ln c_j, 1/c_j} pairs and 1024 {sin, cos} values (the full
+// turn, exact quadrant symmetry), 33 KB with the exp2 table.  About 38 VALU
+// per pair.  A 128-bit Philox block carries one pair and a 32-bit word
+// (the threshold lead of the one-lane and lane-group kernels); the lane-pair
+// kernel packs 5 pairs and two 16-bit leads into 4 blocks.  Accuracy:
+// tests/test_gpu_normals.py (libm form, NumPy).
 // ---------------------------------------------------------------------------
-constexpr int kBm64LogN = 1025, kBm64ScN = 257, kExp2N = 64;
+constexpr int kBm64LogN = 1025, kBm64ScN = 1024, kExp2N = 64;
 constexpr int kBm64ExpOff = 2 * (kBm64LogN + kBm64ScN);   // 2^(i/64) table
-constexpr int kBm64Doubles = kBm64ExpOff + kExp2N;         // 2628 doubles
+constexpr int kBm64Doubles = kBm64ExpOff + kExp2N;         // 4162 doubles
 
 __device__ __forceinline__ uint32_t hi32(double v) {
   return (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32);
@@ -265,66 +273,70 @@ __device__ __forceinline__ void bm64_load(double *lds, const double *g) {
   __syncthreads();
 }
 
-__device__ __forceinline__ void bm64_pair(uint32_t x, uint32_t y, uint32_t z,
-                                          uint32_t w, const double *tab,
-                                          double &z0, double &z1) {
-  // ---- E = -2 ln u1 ----
-  const double d1 = from_words(0x3FF00000u | (x & 0xFFFFFu), y);   // [1, 2)
-  const double u1 = d1 - (1.0 - 0x1p-53);                          // exact (Sterbenz)
-  const uint32_t uh = hi32(u1);
-  const int e1 = (int)((uh >> 20) & 0x7FFu) - 1022;                // exponent + 1
-  const uint32_t mh = 0x3FF00000u | (uh & 0xFFFFFu);
-  const uint32_t ch = (mh + 0x200u) & 0xFFFFFC00u;                 // c_j (hi word)
-  const double2 lt = reinterpret_cast<const double2 *>(tab)[(ch - 0x3FF00000u) >> 10];
-  const double r = (from_words(mh, lo32(u1)) - from_words(ch, 0u)) * lt.y;
+// -2 ln(m 2^e) + offsets for the log table: x = m 2^e (frexp, m in [1/2, 1)),
+// c = m rounded to 10 fraction bits, returns r = (m - c) / c and the table
+// row {-2 ln c, 1/c}; q4 is -2 log1p(r) / r to degree 4.
+struct LogTerm { double r, T; int e; };
+
+__device__ __forceinline__ LogTerm log_term(double x, const double *tab) {
+  const double m = __builtin_amdgcn_frexp_mant(x);                 // [1/2, 1)
+  const int e = __builtin_amdgcn_frexp_exp(x);
+  const uint32_t ch = (hi32(m) + 0x200u) & 0xFFFFFC00u;            // c (hi word)
+  // row j = (ch - 0x3FE00000) >> 10: byte offset 16 j = bits [20:6] of ch
+  const double2 lt = *reinterpret_cast<const double2 *>(
+      reinterpret_cast<const char *>(tab) + __builtin_amdgcn_ubfe(ch, 6, 15));
+  return LogTerm{(m - from_words(ch, 0u)) * lt.y, lt.x, e};
+}
+
+__device__ __forceinline__ double q4(double r) {
   double q = __builtin_fma(r, -0.4, 0.5);
   q = __builtin_fma(q, r, -2.0 / 3.0);
   q = __builtin_fma(q, r, 1.0);
-  q = __builtin_fma(q, r, -2.0);
-  const double de = (double)e1;
+  return __builtin_fma(q, r, -2.0);
+}
+
+__device__ __forceinline__ void bm96_pair(uint32_t a, uint32_t b, uint32_t c,
+                                          const double *tab, double &z0,
+                                          double &z1) {
+  // ---- E = -2 ln u1 ----
+  const double d1 = from_words(__builtin_amdgcn_alignbit(0x3FFu, b, 12), a);   // [1, 2)
+  const double u1 = d1 - (1.0 - 0x1p-53);                          // exact (Sterbenz)
+  const LogTerm lt = log_term(u1, tab);
+  const double de = (double)lt.e;
   const double base = __builtin_fma(de, -2.0 * 6.93147180369123816490e-01,
-                                    __builtin_fma(de, -2.0 * 1.90821492927058770002e-10, lt.x));
-  const double E = __builtin_fma(r, q, base);                       // > 0
+                                    __builtin_fma(de, -2.0 * 1.90821492927058770002e-10, lt.T));
+  const double E = __builtin_fma(lt.r, q4(lt.r), base);             // > 0
   // ---- sqrt(E): v_rsq_f64 + two Newton steps ----
   const double yr = __builtin_amdgcn_rsq(E);
   const double hy = 0.5 * yr;
   double rr = E * yr;
   rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
   rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
-  // ---- (sin, cos) of the quarter-turn angle ----
-  const double2 sc = reinterpret_cast<const double2 *>(tab + 2 * kBm64LogN)[(z >> 22) & 0xFFu];
-  const double d2 = from_words(0x43300000u | (z & 0xFFFFFu), w);    // 2^52 + k2
-  constexpr double kC = 3.14159265358979323846 * 0x1p-61;   // (pi/2) 2^-8 2^-52
-  const double th = __builtin_fma(d2, kC, -kC * 4503599627370496.0);
+  // ---- (sin, cos) of the full-turn angle ----
+  const char *sct = reinterpret_cast<const char *>(tab + 2 * kBm64LogN) + (b & 0xFFCu);
+  const uint32_t *scw = reinterpret_cast<const uint32_t *>(sct);
+  const double2 sc{from_words(scw[kBm64ScN], scw[0]),
+                   from_words(scw[3 * kBm64ScN], scw[2 * kBm64ScN])};
+  constexpr double kTh = 3.14159265358979323846 * 0x1p-41;   // 2 pi 2^-10 2^-32
+  const double th = (double)c * kTh;                          // [0, pi/512)
   const double f = th * th;
   const double ps = __builtin_fma(f, 8.3333333333333333333e-03, -1.6666666666666666667e-01);
   const double st = __builtin_fma(th * f, ps, th);
   const double ct = __builtin_fma(f, __builtin_fma(f, 4.1666666666666666667e-02, -0.5), 1.0);
   const double sn = __builtin_fma(sc.x, ct, sc.y * st);
   const double cs = __builtin_fma(sc.y, ct, -(sc.x * st));
-  const double a0 = rr * cs, a1 = rr * sn;
-  z0 = from_words(hi32(a0) ^ (z & 0x80000000u), lo32(a0));
-  z1 = from_words(hi32(a1) ^ ((z << 1) & 0x80000000u), lo32(a1));
+  z0 = rr * cs;
+  z1 = rr * sn;
 }
 
-// ln S of a positive normal double from the same LDS log table: S = 2^e m,
-// c_j = m rounded to 10 mantissa bits, ln S = (e + 1) ln 2 - (T_j + r q(r)) / 2
-// with T_j = -2 ln(c_j / 2), r = (m - c_j) / c_j (q as in bm64_pair).  About
-// 20 VALU; absolute error ~1e-16 (relative near S = 1 is not kept: used for
-// log-sum-exp sums S in [1, K], added to the max).
+// ln S of a positive normal double from the same LDS log table: S = m 2^e,
+// ln S = e ln 2 - (T_j + r q(r)) / 2 (log_term).  About 18 VALU; absolute
+// error ~1e-16 (relative near S = 1 is not kept: used for log-sum-exp sums
+// S in [1, K], added to the max).
 __device__ __forceinline__ double ln_tab(double S, const double *tab) {
-  const uint32_t sh = hi32(S);
-  const int e1 = (int)((sh >> 20) & 0x7FFu) - 1022;
-  const uint32_t mh = 0x3FF00000u | (sh & 0xFFFFFu);
-  const uint32_t ch = (mh + 0x200u) & 0xFFFFFC00u;
-  const double2 lt = reinterpret_cast<const double2 *>(tab)[(ch - 0x3FF00000u) >> 10];
-  const double r = (from_words(mh, lo32(S)) - from_words(ch, 0u)) * lt.y;
-  double q = __builtin_fma(r, -0.4, 0.5);
-  q = __builtin_fma(q, r, -2.0 / 3.0);
-  q = __builtin_fma(q, r, 1.0);
-  q = __builtin_fma(q, r, -2.0);
-  const double de = (double)e1;
-  const double h = -0.5 * __builtin_fma(r, q, lt.x);
+  const LogTerm lt = log_term(S, tab);
+  const double de = (double)lt.e;
+  const double h = -0.5 * __builtin_fma(lt.r, q4(lt.r), lt.T);
   return __builtin_fma(de, 6.93147180369123816490e-01,
                        __builtin_fma(de, 1.90821492927058770002e-10, h));
 }
@@ -346,11 +358,6 @@ __device__ __forceinline__ double exp_tab(double y, const double *tab) {
   const int ki = (int)k;
   const double t = tab[kBm64ExpOff + (ki & 63)];
   return __builtin_ldexp(t * p, ki >> 6);
-}
-
-// The 14 spare bits of a bm64_pair block: x[31:20] << 2 | z[21:20].
-__device__ __forceinline__ uint32_t bm64_spare(uint32_t x, uint32_t z) {
-  return ((x >> 20) << 2) | ((z >> 20) & 3u);
 }
 
 // Trace store through a buffer resource: base = a wave-uniform (SGPR)
@@ -711,18 +718,22 @@ struct Decision { bool acc, need; };
 // LB = number of leading bits of t known to the filter: t lies in
 // [lead 2^-LB, (lead + 1) 2^-LB).  The lane-pair kernel's Philox path packs a
 // 14-bit lead beside its normals (its fallback draws the remaining bits).
+// The comparison runs in units of 2^-LB: eL = e 2^LB = 2^(fp32(log2e (lp' -
+// lp) + LB)), so t < e (1 - 4e-6) is proven by lead + 1 <= eL (1 - 4e-6)
+// (one fp32 fma: lead <= eL (1 - 4e-6) - 1, rounding 2^-24 eL) and t > e (1 +
+// 4e-6) by lead > eL (1 + 4e-6).  Where a decision can hinge on e (e in
+// [2^-LB, 1]) the argument is in [0, LB]: its fp32 rounding costs at most
+// 4.2e-8 LB relative, as before.
 template <int LB>
 __device__ __forceinline__ Decision accept_filter_lead(double lpp, double lp,
                                                        uint32_t lead, bool lin) {
-  constexpr float w = 1.0f / (float)(1u << LB);
-  const float e = __builtin_amdgcn_exp2f(
-      (float)((lpp - lp) * 1.4426950408889634));
-  const float tlo = (float)lead * w;
-  const float thi = tlo + w;
+  const float eL = __builtin_amdgcn_exp2f(
+      (float)__builtin_fma(lpp - lp, 1.4426950408889634, (double)LB));
+  const float fl = (float)lead;
   const bool inr = !lin && __builtin_fabs(lpp) <= 700. &&
                    __builtin_fabs(lp) <= 700.;
-  const bool af = thi <= e * 0.999996f;
-  const bool rf = tlo > e * 1.000004f;
+  const bool af = fl <= __builtin_fmaf(eL, 0.999996f, -1.0f);
+  const bool rf = fl > eL * 1.000004f;
   return Decision{inr && af, !(inr && (af || rf))};
 }
 

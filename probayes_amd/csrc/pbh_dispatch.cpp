@@ -1,6 +1,7 @@
 // pbh_dispatch.cpp -- runtime dim -> compiled kernel instantiation.
 // The kernels are instantiated per dimension in pbh_inst_*.hip so that the
 // gfx950 code objects compile in parallel.
+#include <cstring>
 #include <cmath>
 
 #include "pbh_kernels.h"
@@ -273,30 +274,46 @@ hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
   return hipGetLastError();
 }
 
-// The bm64 tables (pbh_device.h): {-2 ln(c_j / 2), 1 / c_j} for c_j = 1 + j /
-// 1024, j = 0..1024, then {sin, cos}(j (pi/2) / 256), j = 0..256, then
-// 2^(i/64), i = 0..63.  Evaluated
-// in long double (64-bit significand) and rounded once to double.
+// The bm64 tables (pbh_device.h): {-2 ln c_j, 1 / c_j} for c_j = (1024 + j) /
+// 2048, j = 0..1024, then sin(J 2 pi / 1024) and cos(J 2 pi / 1024), J =
+// 0..1023 (the first quadrant evaluated, the others by exact symmetry) as
+// four arrays of 32-bit words (sin lo, sin hi, cos lo, cos hi), then
+// 2^(i/64), i = 0..63.  Evaluated in long double (64-bit significand) and
+// rounded once to double.
 void bm64_tables(double *out) {
   for (int j = 0; j < kBm64LogN; ++j) {
-    const double c = 1.0 + j / 1024.0;   // exact
-    out[2 * j] = (double)(-2.0L * logl((long double)c / 2.0L));
+    const double c = (1024 + j) / 2048.0;   // exact
+    out[2 * j] = (double)(-2.0L * logl((long double)c));
     out[2 * j + 1] = 1.0 / c;
   }
   const long double pi = 3.141592653589793238462643383279502884L;
-  double *sc = out + 2 * kBm64LogN;
-  for (int j = 0; j < kBm64ScN; ++j) {
-    const long double t = pi / 2.0L * (long double)j / 256.0L;
-    sc[2 * j] = (double)sinl(t);
-    sc[2 * j + 1] = (double)cosl(t);
+  uint32_t *sc = reinterpret_cast<uint32_t *>(out + 2 * kBm64LogN);
+  constexpr int N = kBm64ScN, Q = kBm64ScN / 4;   // entries, per quadrant
+  auto put = [&](int J, double s, double c) {
+    uint64_t bs, bc;
+    memcpy(&bs, &s, 8);
+    memcpy(&bc, &c, 8);
+    sc[J] = (uint32_t)bs;
+    sc[N + J] = (uint32_t)(bs >> 32);
+    sc[2 * N + J] = (uint32_t)bc;
+    sc[3 * N + J] = (uint32_t)(bc >> 32);
+  };
+  for (int j = 0; j < Q; ++j) {
+    const long double t = pi / 2.0L * (long double)j / (long double)Q;
+    const double s = j == 0 ? 0.0 : (double)sinl(t);
+    const double c = j == 0 ? 1.0 : (double)cosl(t);
+    // angle J = j + k Q: (sin, cos) rotated by k quarter turns
+    put(j, s, c);
+    put(j + Q, c, -s);
+    put(j + 2 * Q, -s, -c);
+    put(j + 3 * Q, -c, s);
   }
-  sc[2 * 256] = 1.0;   // sin(pi/2), cos(pi/2) = 0 exactly
-  sc[2 * 256 + 1] = 0.0;
   for (int i = 0; i < kExp2N; ++i) out[kBm64ExpOff + i] = (double)exp2l(i / 64.0L);
 }
 
-// Diagnostic: bm64_pair against the same construction through ocml's libm
-// log / sqrt / sincos (u1 and the angle formed exactly as bm64_pair forms them).
+// Diagnostic: bm96_pair (one pair per 3 words) against the same
+// construction through ocml's libm log / sqrt / sincos (u1 and the angle
+// formed exactly as bm96_pair forms them).
 __global__ void check_normals64_kernel(int64_t n, const uint32_t *words,
                                        const double *tab, double *fast,
                                        double *ref) {
@@ -304,17 +321,15 @@ __global__ void check_normals64_kernel(int64_t n, const uint32_t *words,
   bm64_load(s_bmt, tab);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t x = words[4 * i], y = words[4 * i + 1], z = words[4 * i + 2],
-                 w = words[4 * i + 3];
-  bm64_pair(x, y, z, w, s_bmt, fast[2 * i], fast[2 * i + 1]);
-  const double u1 = from_words(0x3FF00000u | (x & 0xFFFFFu), y) - (1.0 - 0x1p-53);
-  const double k2 = from_words(0x43300000u | (z & 0xFFFFFu), w) - 4503599627370496.0;
-  const double turn = ((double)((z >> 22) & 0xFFu) + k2 * 0x1p-52) * (1.0 / 1024.0);
+  const uint32_t a = words[3 * i], b = words[3 * i + 1], c = words[3 * i + 2];
+  bm96_pair(a, b, c, s_bmt, fast[2 * i], fast[2 * i + 1]);
+  const double u1 = from_words(0x3FF00000u | (b >> 12), a) - (1.0 - 0x1p-53);
+  const double turn = ((double)((b >> 2) & 0x3FFu) + (double)c * 0x1p-32) * (1.0 / 1024.0);
   double sv, cv;
   sincospi(2.0 * turn, &sv, &cv);   // turn of 2 pi
   const double r = sqrt(-2.0 * log(u1));
-  ref[2 * i] = ((z >> 31) & 1u) ? -(r * cv) : r * cv;
-  ref[2 * i + 1] = ((z >> 30) & 1u) ? -(r * sv) : r * sv;
+  ref[2 * i] = r * cv;
+  ref[2 * i + 1] = r * sv;
 }
 
 hipError_t launch_check_normals64(int64_t n, const uint32_t *words,

@@ -51,6 +51,8 @@ struct pbh_engine {
   bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
+  bool mt_stale = false;       // pbh_restore ran: the streams wait for
+                               // pbh_set_legacy_state (the checkpoint's)
   // trace
   int64_t cap = 0;
   int32_t thin = 1, debug = 0;
@@ -397,11 +399,14 @@ int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
   std::vector<double> blk;
   size_t oloc = 0, oscl = 0, olen = 0, odel = 0;
   uint64_t vmode = 0;
+  int32_t ploc_zero = 0;
   e->draw_order.assign(d, 0);
   for (int i = 0; i < d; ++i) e->draw_order[i] = i;
   switch (p->kind) {
     case PBH_PROP_GAUSS: {
       if (!p->loc || !p->scale) return fail(PBH_ERR_ARG, "GAUSS needs loc, scale");
+      ploc_zero = 1;
+      for (int i = 0; i < d; ++i) ploc_zero &= p->loc[i] == 0.0 ? 1 : 0;
       oloc = pack(blk, p->loc, d);
       oscl = pack(blk, p->scale, d);
       if (p->order) {
@@ -477,6 +482,7 @@ int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
   k.bnd_on = bnd_on; k.bnd_xlo = bxlo; k.bnd_xhi = bxhi;
   k.blo = e->dprop + oblo; k.bhi = e->dprop + obhi;
   k.ploc = e->dprop + oloc; k.pscl = e->dprop + oscl;
+  k.ploc_zero = ploc_zero;
   k.plen = e->dprop + olen; k.pdel = e->dprop + odel;
   k.sdelta = p->delta;
   k.ptf = p->tfun ? e->dprop + otf : nullptr;
@@ -680,6 +686,7 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->mt_db = e->legacy_db;   // the state layout is fixed at seeding
+  e->mt_stale = false;
   int rc = dalloc(e->mt_key, (size_t)(e->mt_db ? 2 : 1) * 624 * n);
   if (!rc) rc = dalloc(e->mt_pos, n);
   if (!rc) rc = dalloc(e->mt_has, n);
@@ -702,6 +709,9 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
 int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first");
+  if (e->mt_stale)
+    return fail(PBH_ERR_STATE, "pbh_restore ran after pbh_legacy_seed: set the "
+                "checkpoint's legacy state (pbh_set_legacy_state) first");
   int32_t R = 0;
   int rc = pbh_stream_width(e, &R);
   if (rc) return rc;
@@ -1010,8 +1020,14 @@ int pbh_get_checkpoint(pbh_engine *e, double *x, double *lp, int64_t *step,
   if (step) *step = e->g;
   if (has_pred) *has_pred = e->has_pred ? 1 : 0;
   if (xo) {
-    if (e->rng != PBH_RNG_XOSHIRO || !e->xo_seeded)
-      return fail(PBH_ERR_STATE, "no xoshiro state (rng is not XOSHIRO or no run yet)");
+    if (e->rng != PBH_RNG_XOSHIRO)
+      return fail(PBH_ERR_STATE, "no xoshiro state (rng is not XOSHIRO)");
+    HIP_TRY(hipSetDevice(e->device));
+    if (!e->xo_seeded) {   // before the first run: the state pbh_run would seed
+      HIP_TRY(pbh::launch_xo_seed(e->xo, e->n, e->off, e->seed, e->stream));
+      e->xo_seeded = true;
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipMemcpy(xo, e->xo, (size_t)8 * e->n * sizeof(uint32_t),
                       hipMemcpyDeviceToHost));
   }
@@ -1023,8 +1039,6 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
   if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
     return PBH_ERR_ARG;
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
-  if (e->cap > 0 || e->rep)
-    return fail(PBH_ERR_STATE, "pbh_restore goes before pbh_alloc_trace / replay");
   if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
   if (e->rng == PBH_RNG_XOSHIRO && !xo)
     return fail(PBH_ERR_ARG, "XOSHIRO needs the generator state xo");
@@ -1046,6 +1060,78 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
   e->g = step;
   e->has_pred = has_pred != 0;
   e->gq_valid = false;   // the production Gibbs kernel recomputes g, Q from x
+  e->cap = 0;            // a trace / replay rows of the engine are detached
+  e->rep_steps = 0;
+  e->rep_g0 = step;
+  // device legacy streams: their state is not in x / lp / step; until the
+  // checkpoint's is set (pbh_set_legacy_state) the streams refuse to draw
+  e->mt_stale = e->mt_key != nullptr;
+  return PBH_OK;
+}
+
+int pbh_set_chains(pbh_engine *e, const double *x, const double *lp,
+                   int64_t step, int32_t has_pred) {
+  if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
+    return PBH_ERR_ARG;
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
+  const int64_t n = e->n;
+  const int d = e->d;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  std::vector<double> xt((size_t)n * d);
+  for (int64_t c = 0; c < n; ++c)
+    for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = x[(size_t)c * d + k];
+  HIP_TRY(hipMemcpy(e->x, xt.data(), xt.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->lp, lp, n * sizeof(double), hipMemcpyHostToDevice));
+  e->g = step;
+  e->has_pred = has_pred != 0;
+  e->gq_valid = false;
+  e->cap = 0;            // the trace and the replay rows are detached
+  e->rep_steps = 0;
+  e->rep_g0 = step;
+  return PBH_OK;
+}
+
+int pbh_legacy_state_words(pbh_engine *e, int64_t *words) {
+  if (check_ptr(e, "engine") || check_ptr(words, "words")) return PBH_ERR_ARG;
+  *words = e->mt_key ? (e->mt_db ? 2 : 1) * 624 : 0;
+  return PBH_OK;
+}
+
+int pbh_get_legacy_state(pbh_engine *e, uint32_t *key, int32_t *pos,
+                         int32_t *has, double *gauss) {
+  if (check_ptr(e, "engine") || check_ptr(key, "key") || check_ptr(pos, "pos") ||
+      check_ptr(has, "has") || check_ptr(gauss, "gauss"))
+    return PBH_ERR_ARG;
+  if (!e->mt_key) return fail(PBH_ERR_STATE, "no legacy streams (pbh_legacy_seed)");
+  if (e->mt_stale) return fail(PBH_ERR_STATE, "legacy state stale after pbh_restore");
+  const int64_t n = e->n;
+  const size_t kw = (size_t)(e->mt_db ? 2 : 1) * 624 * n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(key, e->mt_key, kw * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(pos, e->mt_pos, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(has, e->mt_has, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(gauss, e->mt_gauss, n * sizeof(double), hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_set_legacy_state(pbh_engine *e, const uint32_t *key, const int32_t *pos,
+                         const int32_t *has, const double *gauss) {
+  if (check_ptr(e, "engine") || check_ptr(key, "key") || check_ptr(pos, "pos") ||
+      check_ptr(has, "has") || check_ptr(gauss, "gauss"))
+    return PBH_ERR_ARG;
+  if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first (the layout)");
+  const int64_t n = e->n;
+  const size_t kw = (size_t)(e->mt_db ? 2 : 1) * 624 * n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->mt_key, key, kw * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->mt_pos, pos, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->mt_has, has, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->mt_gauss, gauss, n * sizeof(double), hipMemcpyHostToDevice));
+  e->mt_stale = false;
   return PBH_OK;
 }
 
@@ -1402,13 +1488,13 @@ int pbh_check_normals64(int device, int64_t n, const uint32_t *words,
   pbh::bm64_tables(tab.data());
   uint32_t *dw = nullptr;
   double *df = nullptr, *dr = nullptr, *dt = nullptr;
-  int rc = dalloc(dw, 4 * n);
+  int rc = dalloc(dw, 3 * n);
   if (!rc) rc = dalloc(df, 2 * n);
   if (!rc) rc = dalloc(dr, 2 * n);
   if (!rc) rc = dalloc(dt, tab.size());
   hipError_t err = hipSuccess;
   if (!rc) {
-    err = hipMemcpy(dw, words, 4 * n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    err = hipMemcpy(dw, words, 3 * n * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (err == hipSuccess)
       err = hipMemcpy(dt, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice);
     if (err == hipSuccess) err = pbh::launch_check_normals64(n, dw, dt, df, dr);

@@ -46,6 +46,8 @@ struct KArgs {
   // ---- proposal ----
   int32_t prop;
   const double *ploc, *pscl, *plen, *pdel;
+  int32_t ploc_zero;  // GAUSS: every loc is 0 (the production lane-pair
+                      // kernel then forms x + z scale as one fma)
   double sdelta;
   const double *ptf;  // covariance RW: delta' = ptf[d][d] . delta (rf.py:340-354)
   int32_t has_tfun;
@@ -123,7 +125,7 @@ hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
 bool mh_dim_supported(int d);
 hipError_t launch_check_normals(int64_t n, const uint32_t *words, double *fast,
                                 double *ref);
-// bm64_pair (the production fp64 normals) and its libm form on n blocks.
+// bm96_pair (the production fp64 normals) and its libm form on n word triples.
 hipError_t launch_check_normals64(int64_t n, const uint32_t *words,
                                   const double *tab, double *fast, double *ref);
 // per-chain sums / sums of squares / accept counts of trace records

@@ -112,6 +112,37 @@ __device__ __forceinline__ u32x4 ctr(uint32_t j, int64_t g, int64_t chain) {
                    ((uint32_t)((uint64_t)g >> 32) << 16)};
 }
 
+// Production Gaussian draws of one chain-step (mh_kernel and the GMM
+// lane-group / quad kernels draw this same stream): the words of Philox
+// blocks ctr(q, g, chain), q = 0, 1, ..., in order (x, y, z, w); normal pair
+// p takes words 3p .. 3p + 2 (bm96_pair), and the word after the last pair
+// gives the threshold's leading kStepLead bits.  D <= 2: one block per step.
+constexpr int kStepLead = 24;
+
+template <int D>
+__device__ __forceinline__ uint32_t step_draws(const KArgs &a, int64_t g,
+                                               int64_t chain, const double *tab,
+                                               double (&r)[D]) {
+  constexpr int NP = (D + 1) / 2, NW = 3 * NP + 1, NB = (NW + 3) / 4;
+  uint32_t w[4 * NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const u32x4 b = philox4x32_10(ctr(q, g, chain), a.seed_lo, a.seed_hi);
+    w[4 * q] = b.x;
+    w[4 * q + 1] = b.y;
+    w[4 * q + 2] = b.z;
+    w[4 * q + 3] = b.w;
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    double z0, z1;
+    bm96_pair(w[3 * p], w[3 * p + 1], w[3 * p + 2], tab, z0, z1);
+    r[2 * p] = z0;
+    if (2 * p + 1 < D) r[2 * p + 1] = z1;
+  }
+  return w[3 * NP] >> (32 - kStepLead);
+}
+
 // ---------------------------------------------------------------------------
 // Joint density of x' (in the pscale of the model)
 // ---------------------------------------------------------------------------
@@ -468,14 +499,13 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
       thr = row[(int64_t)D * a.n];
     } else if (RNG == PBH_RNG_XOSHIRO) {
-      // two words per normal pair / per 53-bit uniform, in draw order
+      // three words per normal pair, two per 53-bit uniform, in draw order
       if (prop == PBH_PROP_GAUSS) {
 #pragma unroll
         for (int p = 0; p < (D + 1) / 2; ++p) {
-          const uint32_t w0 = xo_next(xs), w1 = xo_next(xs);
-          const uint32_t w2 = xo_next(xs), w3 = xo_next(xs);
+          const uint32_t w0 = xo_next(xs), w1 = xo_next(xs), w2 = xo_next(xs);
           double z0, z1;
-          bm64_pair(w0, w1, w2, w3, s_bmt, z0, z1);
+          bm96_pair(w0, w1, w2, s_bmt, z0, z1);
           r[2 * p] = z0;
           if (2 * p + 1 < D) r[2 * p + 1] = z1;
         }
@@ -490,24 +520,16 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       tw1 = xo_next(xs);
       thr = u01(tw0, tw1);
     } else if (TAB && prop == PBH_PROP_GAUSS) {
-      // one bm64 fp64 normal pair per Philox block; t's leading 14 bits are
-      // block 0's spare bits, the rest come from block 0x40 -- the same t
-      // as the multi-lane GMM kernel's (its lead + fallback block).  The
-      // filter needs only the lead: block 0x40 is drawn when it cannot decide.
-#pragma unroll
-      for (int p = 0; p < (D + 1) / 2; ++p) {
-        const u32x4 w = philox4x32_10(ctr(p, g, chain), a.seed_lo, a.seed_hi);
-        double z0, z1;
-        bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
-        r[2 * p] = z0;
-        if (2 * p + 1 < D) r[2 * p + 1] = z1;
-        if (p == 0) lead = bm64_spare(w.x, w.z);
-      }
-      lead_bits = 14;
+      // bm96 fp64 normal pairs (step_draws); t's leading 24 bits follow the
+      // pairs' words, the rest come from block 0x40 -- the same t as the
+      // multi-lane GMM kernels' (their lead + fallback block).  The filter
+      // needs only the lead: block 0x40 is drawn when it cannot decide.
+      lead = step_draws<D>(a, g, chain, s_bmt, r);
+      lead_bits = kStepLead;
       lead_ctr = 0x40u;
       if (!simple) {
         const u32x4 w = philox4x32_10(ctr(lead_ctr, g, chain), a.seed_lo, a.seed_hi);
-        tw0 = (lead << 18) | (w.x >> 14);
+        tw0 = (lead << (32 - kStepLead)) | (w.x >> kStepLead);
         tw1 = w.y;
         thr = u01(tw0, tw1);
       }
@@ -651,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       // the ratio form's decision through the filter (see mh_pair_kernel);
       // a constant tuple tran scales both log-probs by q~ (App. A-1)
       const double bA = lpp * a.acc_beta, bB = lp * a.acc_beta;
-      const Decision dc = lead_bits == 14 ? accept_filter_lead<14>(bA, bB, lead, lin)
+      const Decision dc = lead_bits == kStepLead ? accept_filter_lead<kStepLead>(bA, bB, lead, lin)
                         : lead_bits == 22 ? accept_filter_lead<22>(bA, bB, lead, lin)
                                           : accept_filter(bA, bB, tw0, lin);
       acc = dc.acc;
@@ -833,16 +855,17 @@ __device__ __forceinline__ double part_max(double v) {
 
 
 // Production draws of a PAIR of steps (2P, 2P + 1) for one lane half: H
-// normals per step.  PHILOX: H Philox blocks q < H (counter q + 16 h), one
-// bm64 fp64 Box-Muller pair each -- normals 0..H-1 feed step A, H..2H-1
-// step B -- and the steps' threshold leads from the blocks' spare bits
-// (LB = 24 bits from two blocks at H >= 4, else 14 from one).  PHILOX_FP32
-// (comparison mode): the round-1 fp32 draws, NP = H / 2 blocks of two fp32
-// pairs plus one block holding the odd normals and 14-bit leads.
+// normals per step.  PHILOX: the words of Philox blocks q < NB (counter
+// q + 16 h) in order; bm96 fp64 Box-Muller pair p takes words 3p .. 3p + 2
+// (normals 0..H-1 feed step A, H..2H-1 step B) and word 3H holds the two
+// steps' 16-bit threshold leads: 3H + 1 words, so at H = 5 (cfg2) the 10
+// normals and both leads of the step pair fill exactly 4 blocks.
+// PHILOX_FP32 (comparison mode): the round-1 fp32 draws, NP = H / 2 blocks
+// of two fp32 pairs plus one block holding the odd normals and 14-bit leads.
 template <int H, int RNG>
 struct PairDraw {
   static constexpr bool F32 = RNG == PBH_RNG_PHILOX_FP32;
-  static constexpr int LB = F32 ? ((H % 2 == 1) ? 14 : 24) : (H >= 4 ? 24 : 14);
+  static constexpr int LB = F32 ? ((H % 2 == 1) ? 14 : 24) : 16;
 
   __device__ __forceinline__ static void draw(const KArgs &a, const double *bmt,
                                               int h, int64_t P, int64_t chain,
@@ -873,13 +896,20 @@ struct PairDraw {
         tb = w.y >> 8;
       }
     } else {
-      uint32_t sp[H];
+      constexpr int NW = 3 * H + 1, NB = (NW + 3) / 4;
+      uint32_t w[4 * NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const u32x4 b = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
+        w[4 * q] = b.x;
+        w[4 * q + 1] = b.y;
+        w[4 * q + 2] = b.z;
+        w[4 * q + 3] = b.w;
+      }
 #pragma unroll
       for (int q = 0; q < H; ++q) {
-        const u32x4 w = philox4x32_10(ctr(q + 16 * h, P, chain), a.seed_lo, a.seed_hi);
         double z0, z1;
-        bm64_pair(w.x, w.y, w.z, w.w, bmt, z0, z1);
-        sp[q] = bm64_spare(w.x, w.z);
+        bm96_pair(w[3 * q], w[3 * q + 1], w[3 * q + 2], bmt, z0, z1);
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int n = 2 * q + e;
@@ -888,18 +918,13 @@ struct PairDraw {
           else rb[n - H] = z;
         }
       }
-      if constexpr (H >= 4) {
-        ta = (sp[0] << 10) | (sp[1] >> 4);
-        tb = (sp[H - 2] << 10) | (sp[H - 1] >> 4);
-      } else {
-        ta = sp[0];
-        tb = sp[H - 1];
-      }
+      ta = w[3 * H] >> 16;
+      tb = w[3 * H] & 0xFFFFu;
     }
   }
 };
 
-template <int D, int RNG, bool MOM>
+template <int D, int RNG, bool MOM, bool LOC0 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_pair_kernel(KArgs a) {
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
@@ -981,14 +1006,13 @@ void mh_pair_kernel(KArgs a) {
       for (int i = 0; i < H; ++i) r[i] = row[(k0 + i) * a.n];
       thr = row[(int64_t)D * a.n];   // used by half 1
     } else if (RNG == PBH_RNG_XOSHIRO) {
-      // this half's stream: four words per fp64 normal pair, then the
+      // this half's stream: three words per fp64 normal pair, then the
       // threshold (drawn by both halves so each stream advances the same)
 #pragma unroll
       for (int p = 0; p < (H + 1) / 2; ++p) {
-        const uint32_t w0 = xo_next(xs), w1 = xo_next(xs);
-        const uint32_t w2 = xo_next(xs), w3 = xo_next(xs);
+        const uint32_t w0 = xo_next(xs), w1 = xo_next(xs), w2 = xo_next(xs);
         double z0, z1;
-        bm64_pair(w0, w1, w2, w3, s_bmt, z0, z1);
+        bm96_pair(w0, w1, w2, s_bmt, z0, z1);
         r[2 * p] = z0;
         if (2 * p + 1 < H) r[2 * p + 1] = z1;
       }
@@ -1009,10 +1033,12 @@ void mh_pair_kernel(KArgs a) {
       t1 = w.y;
     }
     // proposal of this half's dims (scipy rvs: z * scale + loc)
+    // (LOC0, production: every loc is 0, x' = fma(z, scale, x))
     double xp[H];
 #pragma unroll
     for (int i = 0; i < H; ++i)
-      xp[i] = FAST ? x[i] + __builtin_fma(r[i], psc[i], plc[i])
+      xp[i] = LOC0 ? __builtin_fma(r[i], psc[i], x[i])
+            : FAST ? x[i] + __builtin_fma(r[i], psc[i], plc[i])
                    : x[i] + (r[i] * psc[i] + plc[i]);
     // density: Python sum from 0, dims in order, split across the pair
     double lpp;
@@ -1027,7 +1053,7 @@ void mh_pair_kernel(KArgs a) {
       }
       double lo, up;
       halves_f64(p0 + p1, lo, up);   // the two halves' sums, in every lane
-      lpp = -((lo + up) + a.ksum);
+      lpp = (-(lo + up)) - a.ksum;   // = -((lo + up) + ksum) exactly, one op
     } else {
       double tm[H];
 #pragma unroll
@@ -1054,9 +1080,10 @@ void mh_pair_kernel(KArgs a) {
       const Decision dc = PHX ? accept_filter_lead<PD::LB>(lpp, lp, t0, lin)
                               : accept_filter(lpp, lp, t0, lin);
       acc = first || dc.acc;
-      const bool need = hi && !first && dc.need;
-      if (__ballot(need)) {   // wave-uniform, rare
-        if (need) {
+      // half 1's undecided lanes (scalar mask ops; first is wave-uniform)
+      const uint64_t needm = first ? 0ull : __ballot(dc.need) & 0xFFFFFFFF00000000ull;
+      if (needm) {   // wave-uniform, rare
+        if (__builtin_amdgcn_inverse_ballot_w64(needm)) {
           double t;
           if (PHX) {
             // t's remaining 53 - LB bits from a block of this step alone
@@ -1184,8 +1211,8 @@ void mh_pair_kernel(KArgs a) {
 // SIMDs idle at 32 768 chains; here one chain is a group of L lanes (rows of
 // 64 / L lanes) holding the whole state.
 //  * Draws: steps come in aligned groups of L (absolute step / L), and part
-//    p of a group draws step L G + p alone (bm64 fp64 normals + a 14-bit
-//    threshold lead from the block's spare bits); one all-gather over the
+//    p of a group draws step L G + p alone (step_draws: bm96 fp64 normals +
+//    a 24-bit threshold lead); one all-gather over the
 //    group's lanes (v_permlane16/32_swap) hands every lane the L steps'
 //    draws, so each lane runs 1/L of the Philox and Box-Muller work.
 //  * Density: the K components are dealt over the parts (k = p + L kk);
@@ -1251,8 +1278,7 @@ template <int D, int K, int L>
 __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
   constexpr int KL = (K + L - 1) / L;    // component slots per part
   constexpr int CW = 64 / L;             // chains per wavefront
-  constexpr int P = (D + 1) / 2;         // bm64 blocks per step
-  constexpr int LB = 14;                 // threshold lead bits (spare bits)
+  constexpr int LB = kStepLead;          // threshold lead bits (step_draws)
   constexpr double kNegInf = -__builtin_inf();
   __shared__ double s_bmt[kBm64Doubles];
   bm64_load(s_bmt, a.bm64);
@@ -1304,16 +1330,7 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
   for (int64_t G = a.g0 / L; G * L < gend; ++G) {
     // ---- this part's draws for step L G + p, then the group's all-gather
     double rown[D];
-    uint32_t lown = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const u32x4 w = philox4x32_10(ctr(q, G * L + p, chain), a.seed_lo, a.seed_hi);
-      double z0, z1;
-      bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
-      rown[2 * q] = z0;
-      if (2 * q + 1 < D) rown[2 * q + 1] = z1;
-      if (q == 0) lown = bm64_spare(w.x, w.z);
-    }
+    const uint32_t lown = step_draws<D>(a, G * L + p, chain, s_bmt, rown);
     double rall[D][L];
     uint32_t lall[L];
 #pragma unroll
@@ -1438,7 +1455,7 @@ __global__ __launch_bounds__(kBlock) void mh_gmm_lanes_kernel(KArgs a) {
 // (2 per SIMD).  Every exchange inside a chain is a DPP quad_perm move (one
 // VALU per 32-bit word), not a cross-row permlane.
 //  * Draws: aligned groups of 4 steps; lane p draws step 4 G + p alone
-//    (bm64 fp64 normals, a 14-bit threshold lead from the spare bits) and
+//    (step_draws: bm96 fp64 normals, a 24-bit threshold lead) and
 //    the quad broadcasts the group's draws to every lane.
 //  * Density: lane p owns component p; M = max and S = sum of exp(v_k - M)
 //    over the quad (two xor rounds each, the same association in every
@@ -1533,7 +1550,7 @@ __device__ __forceinline__ float qperm_f32(float v) {
 __device__ __attribute__((noinline)) bool gmm_quad_exact(
     const KArgs &a, const double *tab, int64_t g, int64_t chain, uint32_t lead,
     double M, double S, double lm, double ls, double lp0) {
-  constexpr int LB = 14;
+  constexpr int LB = kStepLead;
   const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
   const double t = u01((lead << (32 - LB)) | (w.x >> LB), w.y);
   const double lpp = M + ln_tab(S, tab);
@@ -1551,8 +1568,7 @@ template <int D, int K, bool MOM, bool FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_gmm_quad_kernel(KArgs a) {
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
-  constexpr int P = (D + 1) / 2;         // bm64 blocks per step
-  constexpr int LB = 14;                 // threshold lead bits (spare bits)
+  constexpr int LB = kStepLead;          // threshold lead bits (step_draws)
   __shared__ double s_bmt[kBm64Doubles];
   bm64_load(s_bmt, a.bm64);
   const int lane = threadIdx.x & 63;
@@ -1595,16 +1611,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
     // ---- lane p draws step 4 G + p; the quad shares the group's draws
     double rown[D];
-    uint32_t lown = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const u32x4 w = philox4x32_10(ctr(q, 4 * G + p, chain), a.seed_lo, a.seed_hi);
-      double z0, z1;
-      bm64_pair(w.x, w.y, w.z, w.w, s_bmt, z0, z1);
-      rown[2 * q] = z0;
-      if (2 * q + 1 < D) rown[2 * q + 1] = z1;
-      if (q == 0) lown = bm64_spare(w.x, w.z);
-    }
+    const uint32_t lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
     double gm[4], gs[4];     // the group's states (M, S), for the records
     int64_t grec[4];
     // one step of the group; j is a compile-time constant (DPP controls)
@@ -2360,6 +2367,8 @@ template <int D, bool MOM>
 void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
   if (a.rng == PBH_RNG_REPLAY)
     pbh_launch((mh_pair_kernel<D, PBH_RNG_REPLAY, MOM>), grid, block, 0, st, a);
+  else if (a.rng == PBH_RNG_PHILOX && a.ploc_zero)
+    pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX, MOM, true>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_PHILOX)
     pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX, MOM>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_XOSHIRO)

@@ -298,7 +298,31 @@ class Engine:
               _c.byref(hp),
               None if xo is None else xo.ctypes.data_as(_lib._u32p))
     return {'x': x, 'lp': lp, 'step': step.value, 'has_pred': bool(hp.value),
-            'xo': xo, 'chain_offset': self.chain_offset}
+            'xo': xo, 'mt': self._legacy_state(), 'chain_offset': self.chain_offset}
+
+  def _legacy_state(self):
+    """The device legacy streams' state (key, pos, has, gauss) or None."""
+    words = _c.c_int64()
+    _lib.call('pbh_legacy_state_words', self._h, _c.byref(words))
+    if not words.value:
+      return None
+    key = np.empty((words.value, self.n), np.uint32)
+    pos = np.empty(self.n, np.int32)
+    has = np.empty(self.n, np.int32)
+    gauss = np.empty(self.n)
+    _lib.call('pbh_get_legacy_state', self._h, key.ctypes.data_as(_lib._u32p),
+              pos.ctypes.data_as(_lib._i32p), has.ctypes.data_as(_lib._i32p),
+              _dp(gauss))
+    return {'key': key, 'pos': pos, 'has': has, 'gauss': gauss}
+
+  def set_chains(self, x, lp, step, has_pred):
+    """Replaces the chain state and step anywhere in a run; generator
+    states continue (pbh_set_chains).  The trace and the replay rows are
+    detached: alloc_trace (and upload_replay / legacy_replay) again."""
+    x = np.ascontiguousarray(x, np.float64).reshape(self.n, self.dim)
+    lp = np.ascontiguousarray(lp, np.float64).reshape(self.n)
+    _lib.call('pbh_set_chains', self._h, _dp(x), _dp(lp), _c.c_int64(int(step)),
+              1 if has_pred else 0)
 
   def restore(self, ck):
     """Resume from checkpoint() (after init_chains of the same N and set_rng
@@ -312,6 +336,15 @@ class Engine:
     _lib.call('pbh_restore', self._h, _dp(x), _dp(lp),
               _c.c_int64(int(ck['step'])), 1 if ck['has_pred'] else 0,
               None if xo is None else xo.ctypes.data_as(_lib._u32p))
+    mt = ck.get('mt')
+    if mt is not None:   # device legacy streams continue where they were
+      key = np.ascontiguousarray(mt['key'], np.uint32)
+      pos = np.ascontiguousarray(mt['pos'], np.int32)
+      has = np.ascontiguousarray(mt['has'], np.int32)
+      gauss = np.ascontiguousarray(mt['gauss'], np.float64)
+      _lib.call('pbh_set_legacy_state', self._h, key.ctypes.data_as(_lib._u32p),
+                pos.ctypes.data_as(_lib._i32p), has.ctypes.data_as(_lib._i32p),
+                _dp(gauss))
 
   def trace_len(self):
     r = _c.c_int64()

@@ -17,10 +17,12 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
   device=, thin=, steps_per_launch=.
 """
 import collections
+import warnings
 
 import numpy as np
 import scipy.stats
 
+from probayes_amd import linreg
 from probayes_amd import lower as L
 from probayes_amd import replay
 from probayes_amd.engine import Engine
@@ -67,6 +69,7 @@ class SP:
     self._delta = None     # (delta, args, kwds) or an RF
     self._tfun = None
     self._scores = self._thresh = self._update = None
+    self._samplers = self._counter = self._last = None   # sp.py:113-128
 
   # ---- specification (sp.py:57-100, rf.py:91-304, field.py:220-317) -----
   @property
@@ -480,19 +483,90 @@ class SP:
       form['sym'] = True
     return form
 
+  # ---- sampler registry (sp.py:113-128, 201-258) --------------------------
+  def reset(self, sampler_id=None, reset_last=True):
+    """sp.py:113-128: with no sampler, empties the registry; otherwise the
+    sampler's counter goes to 0 and, with reset_last, its last state is
+    dropped, so that its next step restarts the chains at the sampler's
+    init (step 1 again: auto-accept).  reset_last=False keeps the chains
+    where the last step handed out left them."""
+    if self._samplers is None or sampler_id is None:
+      self._samplers = []
+    if self._counter is None:
+      self._counter = collections.Counter()
+    if self._last is None:
+      self._last = collections.OrderedDict()
+    if sampler_id is None:
+      return None
+    sampler = self.get_sampler(sampler_id)
+    self._counter[sampler] = 0
+    sampler._reset(reset_last)
+    if sampler not in self._last or reset_last:
+      self._last[sampler] = None
+    return self._samplers, self._counter, self._last
+
+  def get_sampler(self, sampler_id=None):
+    """sp.py:201-206: a sampler by index, or the sampler itself."""
+    if sampler_id is None:
+      return self._samplers
+    if type(sampler_id) is int:
+      return self._samplers[sampler_id]
+    return sampler_id
+
+  def get_counter(self, sampler_id=None):
+    """sp.py:208-212: SP steps handed out since the sampler's last reset."""
+    if sampler_id is None:
+      return self._counter
+    return self._counter[self.get_sampler(sampler_id)]
+
+  def get_last(self, sampler_id=None):
+    """sp.py:214-218: the state the sampler's next step proposes from, as an
+    opqr whose p is the chains' current state (None before the first step
+    and after a reset that dropped it)."""
+    if sampler_id is None:
+      return self._last
+    return self._last[self.get_sampler(sampler_id)]
+
+  def next(self, sampler_id, *args, **kwds):
+    """sp.py:221-258: one SP step of the sampler (a Step with the
+    reference's opqrstuv fields).  The sampler keeps its own init, extra
+    and options; args / kwds are accepted for the reference's signature."""
+    sampler = self.get_sampler(sampler_id)
+    if self._counter is None:
+      self.reset()
+    step = sampler._next_step()
+    self._counter[sampler] += sampler.thin
+    self._last[sampler] = OPQR(None, step.v, None, None)
+    return step
+
   # ---- sampling (sp.py:261-295) ---------------------------------------------
   def sampler(self, *args, stop=None, iid=False, joint=False, chains=None,
               seeds=None, rng=None, seed=0, device=0, thin=1,
-              steps_per_launch=0, debug=None):
+              steps_per_launch=0, debug=None, chunk=None):
+    """sp.py:261-278.  stop=n: a bounded generator of n steps (the first
+    step computes all n in one engine run); stop=None: unbounded, computed
+    in chunks of `chunk` steps (default 256) as they are consumed.  A
+    single positional int is the stop, as in the reference."""
+    if self._samplers is None:
+      self.reset()
+    if len(args) == 1 and type(args[0]) is int and stop is None:
+      stop, args = args[0], ()
     init = args[0] if args else None
     extra = args[1] if len(args) > 1 else None
-    if stop is None:
-      raise NotImplementedError('the GPU sampler needs stop=n_steps')
-    return Sampler(self, init, extra, int(stop), iid, joint, chains, seeds,
-                   rng, seed, device, thin, steps_per_launch, debug)
+    sm = Sampler(self, len(self._samplers), init, extra,
+                 None if stop is None else int(stop), iid, joint, chains,
+                 seeds, rng, seed, device, thin, steps_per_launch, debug, chunk)
+    self._samplers.append(sm)
+    self._counter[sm] = 0
+    self._last[sm] = None
+    return sm
 
   def walk(self, sampler, stop=None):
-    """sp.py:281-295."""
+    """sp.py:281-295 (the check after each sample: a walk cut at `stop`
+    draws stop + 1 steps from the sampler, as the reference's does)."""
+    if stop is None and sampler.stop is None:
+      warnings.warn(
+          "No stop specification set - this walk may proceed indefinitely")
     steps = collections.deque()
     for sample in sampler:
       if stop is not None and len(steps) >= stop:
@@ -510,8 +584,9 @@ class SP:
     if not samples or not isinstance(samples[0], Step):
       raise TypeError('SP() summarises samples from SP.sampler()')
     sm = samples[0].sampler
-    idx = np.array([s.i for s in samples])
-    summary = sm.summary(idx)
+    if any(s.sampler is not sm for s in samples):
+      raise AssertionError('Sample must be outputted from sampler: {}'.format(sm))
+    summary = sm.summary(samples)
     if conditionalise:
       for key in ('o', 'p', 'v'):
         pd = getattr(summary, key)
@@ -522,16 +597,32 @@ class SP:
 
 OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',
                                                 'u', 'v'])
+OPQR = collections.namedtuple('opqr', ['o', 'p', 'q', 'r'])
+
+
+class _Block:
+  """Records [0, T) of one engine run of a sampler: trace arrays tr (v_x
+  [N, T, d], v_p [N, T], u [N, T]; debug p_x, p_p, s), thresholds [N, T] or
+  None, the state before record 0 (prev_x [N, d], prev_p [N]), whether
+  record 0 is step 1 of a sampler epoch (first: no predecessor), the global
+  step of its first step (g0), and what a rewind into it needs (rewind)."""
+
+  __slots__ = ('tr', 'thr', 'prev_x', 'prev_p', 'first', 'g0', 'T', 'rewind')
+
+  def __init__(self, tr, thr, prev_x, prev_p, first, g0, rewind):
+    self.tr, self.thr, self.prev_x, self.prev_p = tr, thr, prev_x, prev_p
+    self.first, self.g0, self.rewind = first, g0, rewind
+    self.T = tr['v_x'].shape[1]
 
 
 class Step:
   """One recorded step of a Sampler; fields as the reference's opqrstuv
-  (sp.py:257-258), built lazily from the trace arrays."""
+  (sp.py:257-258), built lazily from its block's trace arrays."""
 
-  __slots__ = ('sampler', 'i')
+  __slots__ = ('sampler', 'block', 'j')
 
-  def __init__(self, sampler, i):
-    self.sampler, self.i = sampler, i
+  def __init__(self, sampler, block, j):
+    self.sampler, self.block, self.j = sampler, block, j
 
   def _pd(self, xs, ps, t):
     sm = self.sampler
@@ -542,44 +633,47 @@ class Step:
 
   @property
   def v(self):
-    return self._pd(self.sampler.tr['v_x'], self.sampler.tr['v_p'], self.i)
+    return self._pd(self.block.tr['v_x'], self.block.tr['v_p'], self.j)
 
   @property
   def p(self):
-    tr = self.sampler.tr
+    tr = self.block.tr
     if 'p_x' not in tr:
       return None
-    return self._pd(tr['p_x'], tr['p_p'], self.i)
+    return self._pd(tr['p_x'], tr['p_p'], self.j)
 
   @property
   def o(self):
-    if self.i == 0:
+    b, j = self.block, self.j
+    if j > 0:
+      return self._pd(b.tr['v_x'], b.tr['v_p'], j - 1)
+    if b.first:
       return None
-    return self._pd(self.sampler.tr['v_x'], self.sampler.tr['v_p'], self.i - 1)
+    return self._pd(b.prev_x[:, None, :], b.prev_p[:, None], 0)
 
   @property
   def u(self):
-    u = self.sampler.tr['u'][:, self.i].astype(bool)
+    u = self.block.tr['u'][:, self.j].astype(bool)
     if self.sampler.batched:
       return u
     return True if u[0] else None
 
   @property
   def s(self):
-    tr = self.sampler.tr
+    tr = self.block.tr
     if 's' not in tr:
       return None
-    v = tr['s'][:, self.i]
+    v = tr['s'][:, self.j]
     if self.sampler.batched:
       return v
     return None if np.isnan(v[0]) else float(v[0])
 
   @property
   def t(self):
-    th = self.sampler.thresholds
+    th = self.block.thr
     if th is None:
       return None
-    return th[:, self.i] if self.sampler.batched else float(th[0, self.i])
+    return th[:, self.j] if self.sampler.batched else float(th[0, self.j])
 
   def astuple(self):
     return OPQRSTUV(self.o, self.p, None, None, self.s, self.t, self.u, self.v)
@@ -588,12 +682,34 @@ class Step:
     return self.astuple()[i]
 
 
-class Sampler:
-  """A lowered, batched MH/Gibbs run of `stop` steps (sp.py:261-278)."""
+class _GlobalStream:
+  """Draws the single-chain legacy stream from NumPy's GLOBAL RandomState
+  ahead of use and keeps the global state exactly where the reference
+  leaves it: states[k] is the global state after step k's draws; handing
+  out step k sets it, and a draw made by anyone else in between (the global
+  state is not states[k - 1] any more) invalidates the steps drawn ahead."""
 
-  def __init__(self, sp, init, extra, stop, iid, joint, chains, seeds, rng,
-               seed, device, thin, steps_per_launch, debug):
-    self.sp, self.init, self.extra = sp, init, extra
+  @staticmethod
+  def state():
+    return np.random.get_state()
+
+  @staticmethod
+  def same(a, b):
+    return a[2:] == b[2:] and np.array_equal(a[1], b[1])
+
+
+class Sampler:
+  """A lowered, batched MH/Gibbs process (sp.py:261-278, sp_utils.py:8-16):
+  an iterator of Steps.  Steps are computed by the engine in blocks (all of
+  a bounded sampler's steps at once, `chunk` steps at a time when
+  unbounded) and handed out one at a time; SP.reset / SP.next / get_last /
+  get_counter act on the steps handed out, rewinding the engine when it ran
+  ahead of them (the counter-based production RNG and the device legacy
+  streams continue exactly as an uninterrupted run would)."""
+
+  def __init__(self, sp, sid, init, extra, stop, iid, joint, chains, seeds,
+               rng, seed, device, thin, steps_per_launch, debug, chunk):
+    self.sp, self.sid, self.init, self.extra = sp, sid, init, extra
     self.stop, self.iid, self.joint = stop, iid, joint
     self.batched = chains is not None
     self.n = int(chains) if self.batched else 1
@@ -602,12 +718,44 @@ class Sampler:
       rng = 'legacy' if (not self.batched or seeds is not None) else 'philox'
     self.rng, self.seed, self.device = rng, seed, device
     self.thin, self.spl = int(thin), int(steps_per_launch)
+    self.chunk = int(chunk) if chunk else 256
+    if self.chunk % self.thin:
+      self.chunk += self.thin - self.chunk % self.thin
     self.debug = (not self.batched) if debug is None else bool(debug)
     self.names = sp.keylist
-    self.tr = None
-    self.thresholds = None
     self.spec = None
+    self._eng = None        # the engine (MH / CondCov Gibbs)
+    self._lx = None         # linreg: the chains' state [N, 3] (host)
+    self._rs = None         # linreg legacy streams: RandomState per chain
+    self._g = 0             # global step of the next step to compute
+    self._cur = None        # block being handed out and its next record
+    self._j = 0
+    self._handed = None     # (block, j) of the last record handed out
+    self._epoch = True      # the next step starts an epoch (at init)
+    self._drawn = []        # (global step, steps) drawn from seeded streams
+    self._done = False      # a bounded sampler ran out (sp_utils.py:14-16)
+    self.blocks = []
 
+  def __repr__(self):
+    return '<probayes_amd Sampler {} stop={}>'.format(self.sid, self.stop)
+
+  def __hash__(self):
+    return id(self)
+
+  # ---- the generator (sp_utils.py:8-16) ------------------------------------
+  def __iter__(self):
+    return self
+
+  def __next__(self):
+    if self._done:
+      raise StopIteration
+    if self.stop is not None and self.sp.get_counter(self) >= self.stop:
+      self.sp.reset(self)
+      self._done = True
+      raise StopIteration
+    return self.sp.next(self)
+
+  # ---- set-up ------------------------------------------------------------
   def _init_array(self):
     d, n = len(self.names), self.n
     init = {_key(k): v for k, v in (self.init or {}).items()}
@@ -617,6 +765,10 @@ class Sampler:
         raise ValueError('init value missing for {}'.format(k))
       out[:, i] = np.broadcast_to(np.asarray(init[k], np.float64), (n,))
     return out
+
+  def _is_gibbs(self):
+    return self.spec.get('kind') == 'linreg' or \
+        self.spec['proposal']['kind'] == 'gibbs'
 
   def _cycle_rf(self):
     """The RF whose conditional cycle this Gibbs run advances: the
@@ -633,137 +785,322 @@ class Sampler:
     p = self.spec['proposal']
     return -(-int(self.spec['dim']) // int(p['tsteps']))
 
-  def run(self):
-    if self.tr is not None:
-      return self
+  def _lower(self):
+    if self.spec is not None:
+      return
     self.spec = self.sp.lower(self.extra, self.iid, self.joint)
     self.pscale = self.spec['pscale']
-    gibbs = self.spec.get('kind') == 'linreg' or \
-        self.spec['proposal']['kind'] == 'gibbs'
-    rf = self._cycle_rf() if gibbs else None
-    self.step0 = getattr(rf, '_pbh_cond_step', 0) if gibbs else 0
-    if self.spec.get('kind') == 'linreg':
-      self._run_linreg()
-    else:
-      self._run_engine()
-    if gibbs:   # the RF's __cond_mod advances by one block per SP step
-      rf._pbh_cond_step = (self.step0 + self.stop) % self._cycle_len()
-    return self
+    if self.rng == 'legacy' and self.batched and self.seeds is None:
+      raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
+    if self.spec.get('kind') == 'linreg' and self.thin != 1:
+      raise L.NotLowerable('linreg Gibbs records every step (thin=1)')
 
-  def _run_engine(self):
-    eng = Engine(self.spec, device=self.device)
-    try:
-      eng.init_chains(self._init_array())
-      if self.step0:
-        eng.set_step(self.step0)
+  def _start_epoch(self):
+    """Chains back at init, step 1 next (auto-accept); a Gibbs cycle starts
+    at its RF's phase; every generator continues."""
+    gibbs = self._is_gibbs()
+    phase = getattr(self._cycle_rf(), '_pbh_cond_step', 0) if gibbs else 0
+    g = self._g
+    if gibbs:   # the next step index at the RF's cycle phase
+      g += (phase - g) % self._cycle_len()
+    init = self._init_array()
+    if self.spec.get('kind') == 'linreg':
+      self._lx = init
+      if self.rng == 'legacy' and self.seeds is not None and self._rs is None:
+        self._rs = [np.random.RandomState(int(s)) for s in
+                    np.asarray(self.seeds).reshape(-1)]
+    elif self._eng is None:
+      eng = Engine(self.spec, device=self.device)
+      self._eng = eng
+      eng.init_chains(init)
+      if g:
+        eng.set_step(g)
       if self.rng == 'legacy':
-        seeds = None if self.seeds is None else np.asarray(self.seeds)
-        if seeds is None and self.batched:
-          raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
         eng.set_rng('replay')
-        if seeds is None:
-          # one chain on NumPy's GLOBAL stream: drawn on the host so that the
-          # global state advances exactly as the reference leaves it
-          streams = replay.legacy_streams(self.spec, self.stop, seeds,
-                                          step0=self.step0)
-          eng.upload_replay(streams)
-          th = streams[:, -1, :] if self.spec['proposal']['kind'] != 'gibbs' \
-              else None
-        else:
+        if self.seeds is not None:
           # RandomState(seeds[c]) per chain, generated on the device
-          eng.seed_legacy(seeds)
-          eng.legacy_replay(self.stop)
-          th = eng.get_replay(0, self.stop, eng.stream_width() - 1) \
-              if self.spec['proposal']['kind'] != 'gibbs' else None
-        if th is not None:
-          self.thresholds = th.T[:, self.thin - 1::self.thin]
+          eng.seed_legacy(np.asarray(self.seeds))
       else:
         eng.set_rng(self.rng, self.seed)
-      eng.alloc_trace(self.stop // self.thin, self.thin, debug=self.debug)
-      eng.run(self.stop, steps_per_launch=self.spl)
-      self.tr = eng.trace()
-      self.moments = eng.moments()
-    finally:
-      eng.close()
+    else:
+      self._eng.set_chains(init, np.zeros(self.n), g, False)
+    self._g = g
+    self._epoch_first = True
 
-  def _run_linreg(self):
-    from probayes_amd import linreg
+  def close(self):
+    """Frees the engine (also done when the sampler is collected)."""
+    if self._eng is not None:
+      self._eng.close()
+      self._eng = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:   # interpreter shutdown
+      pass
+
+  # ---- computing blocks ----------------------------------------------------
+  def _block_steps(self):
+    if self.stop is not None:
+      left = self.stop - self.sp.get_counter(self)
+      if left > 0:
+        return left - left % self.thin if left >= self.thin else self.thin
+    return self.chunk
+
+  def _draw_global(self, k):
+    """k steps of the single chain's legacy stream from NumPy's global
+    state, with the global state after each step."""
+    out, states = [], []
+    for t in range(k):
+      if self.spec.get('kind') == 'linreg':
+        out.append(linreg.legacy_streams(1, len(self.spec['x_obs']),
+                                         self.spec['hyper'][4], None,
+                                         step0=self._g + t))
+      else:
+        out.append(replay.legacy_streams(self.spec, 1, None,
+                                         step0=self._g + t))
+      states.append(_GlobalStream.state())
+    return np.concatenate(out, axis=0), states
+
+  def _compute(self):
+    """Runs the next block from the current chain state."""
+    k = self._block_steps()
+    first = self._epoch_first
+    self._epoch_first = False
+    g0 = self._g
+    rewind = {}
+    if self.spec.get('kind') == 'linreg':
+      tr, thr, prev_x, prev_p = self._compute_linreg(k, rewind)
+    else:
+      tr, thr, prev_x, prev_p = self._compute_engine(k, rewind)
+    self._g = g0 + k
+    b = _Block(tr, thr, prev_x, prev_p, first, g0, rewind)
+    self.blocks.append(b)
+    self._cur, self._j = b, 0
+
+  def _compute_engine(self, k, rewind):
+    eng = self._eng
+    prev_x, prev_p = eng.state()
+    thr = None
+    if self.rng == 'legacy':
+      if self.seeds is None:
+        streams, rewind['states'] = self._draw_global(k)
+        eng.upload_replay(streams)
+        thr = streams[:, -1, :] if self.spec['proposal']['kind'] != 'gibbs' else None
+      else:
+        eng.legacy_replay(k)
+        self._drawn.append((self._g, k))   # steps drawn since seeding
+        thr = eng.get_replay(0, k, eng.stream_width() - 1) \
+            if self.spec['proposal']['kind'] != 'gibbs' else None
+      if thr is not None:
+        thr = thr.T[:, self.thin - 1::self.thin]
+    elif self.rng == 'xoshiro':
+      rewind['ck'] = eng.checkpoint()     # the generators at block start
+    eng.alloc_trace(k // self.thin, self.thin, debug=self.debug)
+    eng.run(k, steps_per_launch=self.spl)
+    return eng.trace(), thr, prev_x, prev_p
+
+  def _compute_linreg(self, k, rewind):
     sp = self.spec
-    if self.thin != 1:
-      raise L.NotLowerable('linreg Gibbs records every step (thin=1)')
     rand, rng = None, self.rng
-    n_obs = len(sp['x_obs'])
     if rng == 'legacy':
-      if self.batched and self.seeds is None:
-        raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
-      rand = linreg.legacy_streams(self.stop, n_obs, sp['hyper'][4],
-                                   None if self.seeds is None else self.seeds,
-                                   step0=self.step0)
+      if self.seeds is None:
+        rand, rewind['states'] = self._draw_global(k)
+      else:
+        rand = self._linreg_draws(self._g, k)
+        self._drawn.append((self._g, k))
       rng = 'replay'
-    out = linreg.run(sp['x_obs'], sp['y_obs'], self._init_array(), self.stop,
-                     hyper=sp['hyper'], vsets=sp['vsets'], rng=rng,
-                     seed=self.seed, rand=rand, device=self.device,
-                     step0=self.step0)
+    prev_x = self._lx
+    out = linreg.run(sp['x_obs'], sp['y_obs'], self._lx, k, hyper=sp['hyper'],
+                     vsets=sp['vsets'], rng=rng, seed=self.seed, rand=rand,
+                     device=self.device, step0=self._g)
     vx, vp = out['v_x'], out['v_p']
+    self._lx = out['final_x']
     # gibbs: p = v, u = True, s = t = None (sp_utils.py:75-84)
-    self.tr = {'v_x': vx, 'v_p': vp, 'p_x': vx, 'p_p': vp,
-               'u': np.ones(vp.shape, np.uint8)}
-    self.moments = None
+    tr = {'v_x': vx, 'v_p': vp, 'p_x': vx, 'p_p': vp,
+          'u': np.ones(vp.shape, np.uint8)}
+    return tr, None, prev_x, np.full(self.n, np.nan)
 
-  def __iter__(self):
-    self.run()
-    for t in range(self.tr['v_x'].shape[1]):
-      yield Step(self, t)
+  def _linreg_draws(self, g, k, keep=True):
+    """k steps from the seeded per-chain RandomStates (linreg's legacy
+    order: standard_gamma on y_sigma steps, gauss otherwise)."""
+    alpha = self.spec['hyper'][4] + 0.5 * len(self.spec['x_obs'])
+    rand = np.empty((k, len(self._rs)))
+    for c, r in enumerate(self._rs):
+      for t in range(k):
+        rand[t, c] = r.standard_gamma(alpha) if (g + t) % 3 == 2 \
+            else r.standard_normal()
+    return rand
 
-  def summary(self, idx=None):
-    self.run()
-    T = self.tr['v_x'].shape[1]
-    idx = np.arange(T) if idx is None else np.asarray(idx)
-    sel = (lambda a: a[0, idx]) if not self.batched else \
-        (lambda a: np.moveaxis(a[:, idx], 0, 1))
+  def _reseed_streams(self, keep):
+    """Rewinds the seeded legacy streams to the draws of the first `keep`
+    steps since seeding: seed again, then draw and discard those steps at
+    their global step indices (the draw kinds and counts of a Gibbs step
+    follow its place in the cycle)."""
+    log, self._drawn = self._drawn, []
+    linreg_ = self.spec.get('kind') == 'linreg'
+    if linreg_:
+      self._rs = [np.random.RandomState(int(s)) for s in
+                  np.asarray(self.seeds).reshape(-1)]
+    else:
+      eng = self._eng
+      eng.seed_legacy(np.asarray(self.seeds))
+      x, p = eng.state()
+    for g, k in log:
+      k = min(k, keep)
+      for b in range(0, k, 256):
+        m = min(256, k - b)
+        if linreg_:
+          self._linreg_draws(g + b, m)
+        else:
+          eng.set_chains(x, p, g + b, True)
+          eng.legacy_replay(m)
+      if k:
+        self._drawn.append((g, k))
+      keep -= k
 
-    def pd(xkey, pkey):
-      if xkey not in self.tr:
+  # ---- handing out steps ---------------------------------------------------
+  def _next_step(self):
+    self._lower()
+    if self._epoch:
+      self._start_epoch()
+      self._epoch = False
+      self._cur = None
+    cur = self._cur
+    if cur is not None and self._j < cur.T and 'states' in cur.rewind and \
+        self._j > 0 and not _GlobalStream.same(
+            _GlobalStream.state(), cur.rewind['states'][self._j * self.thin - 1]):
+      # someone drew from the global stream since the last step: the steps
+      # drawn ahead are not the reference's any more
+      self._rewind_to_handed()
+      cur = None
+    if cur is None or self._j >= cur.T:
+      self._compute()
+      cur = self._cur
+    j = self._j
+    self._j += 1
+    if 'states' in cur.rewind:
+      np.random.set_state(cur.rewind['states'][(j + 1) * self.thin - 1])
+    self._handed = (cur, j)
+    if self._is_gibbs():   # the RF's __cond_mod follows the steps handed out
+      self._cycle_rf()._pbh_cond_step = \
+          (cur.g0 + (j + 1) * self.thin) % self._cycle_len()
+    return Step(self, cur, j)
+
+  def _rewind_to_handed(self):
+    """Puts the chains (and their generators) where the last step handed
+    out left them: the engine may have run ahead of it."""
+    cur = self._cur
+    if cur is None or self._j >= cur.T:
+      return   # nothing ahead
+    b, j = self._handed if self._handed is not None else (cur, -1)
+    if b is not cur:
+      return
+    g = cur.g0 + (j + 1) * self.thin
+    x = cur.prev_x if j < 0 else cur.tr['v_x'][:, j, :]
+    p = cur.prev_p if j < 0 else cur.tr['v_p'][:, j]
+    has_pred = not (j < 0 and cur.first)
+    seeded = self.rng == 'legacy' and self.seeds is not None
+    if seeded:   # the streams: what was drawn before this block + j + 1 steps
+      total = sum(k for _, k in self._drawn)
+      self._reseed_streams(total - cur.T * self.thin + (j + 1) * self.thin)
+    if self.spec.get('kind') == 'linreg':
+      self._lx = np.array(x)
+    elif 'ck' in cur.rewind:
+      # xoshiro: back to the block start, then the handed steps again (the
+      # same draws, the same chains)
+      eng = self._eng
+      eng.restore(cur.rewind['ck'])
+      if j >= 0:
+        eng.run((j + 1) * self.thin, steps_per_launch=self.spl)
+    else:
+      # counter-based draws (Philox) or host streams: the state is all; the
+      # global NumPy state was set when step j was handed out and any draw
+      # made since then is the user's own, which the reference would see too
+      self._eng.set_chains(x, p, g, has_pred)
+    self._g = g
+    self._epoch_first = j < 0 and cur.first
+    self._cur, self._j = None, 0
+
+  def _reset(self, reset_last):
+    """SP.reset: reset_last restarts the chains at init at the next step;
+    otherwise they continue from the last step handed out."""
+    if reset_last:
+      self._epoch = True
+    else:
+      self._rewind_to_handed()
+    self._cur, self._j = None, 0
+
+  # ---- summaries -------------------------------------------------------------
+  def _gather(self, steps, get):
+    """[N, len(steps), ...] from get(block) [N, T, ...] at the steps'
+    records, one fancy index per run of steps from the same block."""
+    parts, i = [], 0
+    while i < len(steps):
+      b = steps[i].block
+      k = i
+      while k < len(steps) and steps[k].block is b:
+        k += 1
+      js = np.array([s.j for s in steps[i:k]])
+      a = get(b)
+      parts.append(None if a is None else a[:, js])
+      i = k
+    if any(p is None for p in parts):
+      return None
+    return np.concatenate(parts, axis=1)
+
+  def summary(self, steps):
+    steps = list(steps)
+    sel = (lambda a: a[0]) if not self.batched else (lambda a: np.moveaxis(a, 0, 1))
+    tr = lambda key: (lambda b: b.tr.get(key))
+
+    def pd(xkey, pkey, subset=None):
+      xs = self._gather(steps if subset is None else subset, tr(xkey))
+      if xs is None:
         return None
-      xs = self.tr[xkey]
+      ps = self._gather(steps if subset is None else subset, tr(pkey))
       vals = {k: sel(xs[..., i]) for i, k in enumerate(self.names)}
-      return PD('p', vals, prob=sel(self.tr[pkey]), pscale=self.pscale)
+      return PD('p', vals, prob=sel(ps), pscale=self.pscale)
 
-    u = sel(self.tr['u']).astype(bool)
+    u = sel(self._gather(steps, tr('u'))).astype(bool)
     if self.batched:
       u = u.view(FlagArray)
     else:
       u = [True if b else None for b in u]
-    s = sel(self.tr['s']) if 's' in self.tr else None
-    t = None if self.thresholds is None else sel(self.thresholds)
+    s_ = self._gather(steps, tr('s'))
+    s = None if s_ is None else sel(s_)
+    t_ = self._gather(steps, lambda b: b.thr)
+    t = None if t_ is None else sel(t_)
     v = pd('v_x', 'v_p')
-    o, q, r = self._oqr(idx, sel)
+    o, q, r = self._oqr(steps, sel)
     return OPQRSTUV(o, pd('p_x', 'p_p'), q, r, s, t, u, v)
 
-  def _oqr(self, idx, sel):
+  def _oqr(self, steps, sel):
     """The summary's o, q and r (sp.py:160-191, sd.py:253-288): o = the
-    predecessor (the last accepted state; None on step 1, so summated over
-    the steps after the first), q = the transition PD over (x', x) with the
-    tran's value as prob, r = the reverse PD over (x, x') for an asymmetric
-    tran, whose value equals q's (rf.py:536, App. A-6).  q and r need the
-    recorded proposals (debug traces; single-chain samplers record them) and
-    are None for Gibbs."""
-    tr, names = self.tr, self.names
+    predecessor (the last accepted state; None on step 1 of an epoch, so
+    summated over the other steps), q = the transition PD over (x', x) with
+    the tran's value as prob, r = the reverse PD over (x, x') for an
+    asymmetric tran, whose value equals q's (rf.py:536, App. A-6).  q and r
+    need the recorded proposals (debug traces; single-chain samplers record
+    them) and are None for Gibbs."""
+    names = self.names
     if self.spec.get('kind') == 'linreg' or self.spec['scores'] == 'gibbs':
       return None, None, None
-    vx, vp = tr['v_x'], tr['v_p']                 # [N, T, d], [N, T]
-    later = idx[idx > 0]
+    # the state before each step: the previous record, or the block's prev
+    prev_x = lambda b: np.concatenate([b.prev_x[:, None, :], b.tr['v_x'][:, :-1]], 1)
+    prev_p = lambda b: np.concatenate([b.prev_p[:, None], b.tr['v_p'][:, :-1]], 1)
+    later = [st for st in steps if not (st.j == 0 and st.block.first)]
     o = None
-    if later.size:
-      sel_o = (lambda a: a[0, later - 1]) if not self.batched else \
-          (lambda a: np.moveaxis(a[:, later - 1], 0, 1))
-      o = PD('p', {k: sel_o(vx[..., i]) for i, k in enumerate(names)},
-             prob=sel_o(vp), pscale=self.pscale)
-    if 'p_x' not in tr:
+    if later:
+      ox = self._gather(later, prev_x)
+      op = self._gather(later, prev_p)
+      o = PD('p', {k: sel(ox[..., i]) for i, k in enumerate(names)},
+             prob=sel(op), pscale=self.pscale)
+    px = self._gather(steps, lambda b: b.tr.get('p_x'))
+    if px is None:
       return o, None, None
-    init = self._init_array()                      # [N, d]
-    prev = np.concatenate([init[:, None, :], vx[:, :-1, :]], axis=1)
-    px = tr['p_x']
+    prev = self._gather(steps, prev_x)
+    vp = self._gather(steps, lambda b: b.tr['v_p'])
     tran = self.spec['tran']
     if self.spec['scores'] == 'metropolis' and self.sp._tran_spec() is None:
       qv = None

@@ -1,12 +1,10 @@
-# Quick GPU iteration: the given pytest targets, then the workload bench.
-# usage: bash scripts/gpu_iter.sh "<pytest targets>" [extra step command]
+# One iteration on the GPU: the -m gpu suite (stops at the first failure),
+# then the headline evidence (scripts/gpu_headline.sh TAG).
+# usage: bash scripts/gpu_iter.sh TAG [pytest selection]
 export TMPDIR=/tmp
-O=$PWD/gpurun_out
-mkdir -p $O
-rm -f $O/iter_*.log
-timeout -k 10 400 python -u -m pytest $1 -x -q -rf -p no:warnings --timeout 120 --timeout-method thread > $O/iter_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/iter_tests.log
-case $rc in 124|134|137|139) exit $rc;; esac
-timeout -k 10 240 python scripts/bench_workloads.py > $O/iter_workloads.log 2>&1 || exit $?
-if [ -n "$2" ]; then timeout -k 10 300 bash -c "$2" > $O/iter_extra.log 2>&1 || exit $?; fi
-echo ok
+TAG=${1:-it}; shift
+mkdir -p gpurun_out/$TAG
+SEL=${@:-tests}
+timeout -k 10 600 python -u -m pytest $SEL -m gpu -x -q -rf -p no:warnings --timeout 120 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 gpurun_out/$TAG/tests.log; exit 1; }
+tail -3 gpurun_out/$TAG/tests.log
+bash scripts/gpu_headline.sh $TAG

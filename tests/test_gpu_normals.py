@@ -58,49 +58,55 @@ def _normals64(words):
   return fast, ref
 
 
-def _bm64_host(w):
-  """bm64_pair's construction in NumPy (pbh_device.h): u1 = (k1 + 1/2)
-  2^-52 from x[19:0]:y, the quarter-turn angle from z[29:22] and z[19:0]:w,
-  signs z[31], z[30]."""
+def _bm96_host(w):
+  """bm96_pair's construction in NumPy (pbh_device.h): u1 = (k1 + 1/2)
+  2^-52 from b[31:12]:a, the full-turn angle (J + c 2^-32) 2 pi / 1024 with
+  J = b[11:2]."""
   w = w.astype(np.uint64)
-  k1 = ((w[:, 0] & 0xFFFFF) << 32) | w[:, 1]
+  k1 = ((w[:, 1] >> 12) << 32) | w[:, 0]
   u1 = (k1.astype(np.float64) + 0.5) * 2.0 ** -52
-  k2 = ((w[:, 2] & 0xFFFFF) << 32) | w[:, 3]
-  j = ((w[:, 2] >> 22) & 0xFF).astype(np.float64)
-  ang = (j + k2.astype(np.float64) * 2.0 ** -52) * (np.pi / 2 / 256)
+  j = ((w[:, 1] >> 2) & 0x3FF).astype(np.float64)
+  ang = (j + w[:, 2].astype(np.float64) * 2.0 ** -32) * (2 * np.pi / 1024)
   r = np.sqrt(-2.0 * np.log(u1))
-  s0 = np.where((w[:, 2] >> 31) & 1, -1.0, 1.0)
-  s1 = np.where((w[:, 2] >> 30) & 1, -1.0, 1.0)
-  return np.stack([s0 * r * np.cos(ang), s1 * r * np.sin(ang)], 1), r
+  return np.stack([r * np.cos(ang), r * np.sin(ang)], 1), r
+
+
+def _words96(rng, n):
+  w = rng.randint(0, 2 ** 32, (n, 3), dtype=np.uint64).astype(np.uint32)
+  # extremes: u1 at 2^-53 (largest r) and 1 - 2^-53 (r -> 0), the
+  # mantissa's round-up to c = 1, angles at the table's rows 0, 255, 256 (a
+  # quarter turn), 1023 and at a row's end
+  w[0, :2] = [0, 0]
+  w[1, :2] = [0xFFFFFFFF, 0xFFFFFFFF]
+  w[2, :2] = [0, 0xFFF00000]
+  w[3, :2] = [0xFFFFFFFF, 0xFFEFFFFF]
+  w[4:10, 1] = (w[4:10, 1] & 0xFFFFF003) | (np.array([0, 255, 256, 1023, 512, 768],
+                                                     np.uint32) << 2)
+  w[4:10, 2] = [0, 0xFFFFFFFF, 0, 0xFFFFFFFF, 0, 1]
+  return w
 
 
 def test_bm64_normals_match_libm_and_numpy():
-  """The production fp64 normals (bm64_pair: 1025-entry log table + degree-5
-  log1p, rsq + Newton sqrt, 256-entry quarter-turn sin/cos table) against the
+  """The production fp64 normals (bm96_pair: 1025-entry log table + degree-5
+  log1p, rsq + Newton sqrt, 1024-entry full-turn sin/cos table) against the
   same construction through ocml's libm and through NumPy on the host:
   within a few ulp (absolute below |z| = 1, relative above)."""
   rng = np.random.RandomState(11)
   n = 1 << 20
-  w = rng.randint(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
-  # extremes: u1 at 2^-53 (largest r) and 1 - 2^-53 (r -> 0), mantissa
-  # round-up to c = 2, angle at the table edges and just below pi/2
-  w[0, :2] = [0, 0]
-  w[1, :2] = [0xFFFFFFFF, 0xFFFFFFFF]
-  w[2, :2] = [0x000FFE00, 0]
-  w[3, :2] = [0x000FFDFF, 0xFFFFFFFF]
-  w[4:8, 2:] = [[0, 0], [0x3FCFFFFF, 0xFFFFFFFF], [0x00F00000, 0],
-                [0xFFCFFFFF, 0xFFFFFFFF]]
+  w = _words96(rng, n)
   fast, ref = _normals64(w)
   assert np.isfinite(fast).all()
   scale = np.maximum(1.0, np.abs(ref))
   assert np.max(np.abs(fast - ref) / scale) < 4e-15
-  host, r = _bm64_host(w)
+  host, r = _bm96_host(w)
   assert np.max(np.abs(fast - host) / np.maximum(1.0, r)[:, None]) < 1e-14
-  # r near 0 keeps relative accuracy (u1 -> 1: ln(c/2) = 0 exactly)
+  # r near 0 keeps relative accuracy (u1 -> 1: ln c = 0 exactly)
   small = r < 1e-3
-  if small.any():
-    rel = np.abs(np.hypot(fast[small, 0], fast[small, 1]) / r[small] - 1)
-    assert rel.max() < 1e-14
+  assert small.any()
+  rel = np.abs(np.hypot(fast[small, 0], fast[small, 1]) / r[small] - 1)
+  assert rel.max() < 1e-14
+  # the largest radius: u1 = 2^-53
+  assert abs(np.hypot(*fast[0]) - np.sqrt(2 * 53 * np.log(2.0))) < 1e-13
 
 
 def test_bm64_normals_are_standard_normal():
@@ -109,7 +115,7 @@ def test_bm64_normals_are_standard_normal():
   import scipy.stats
   rng = np.random.RandomState(5)
   n = 1 << 22
-  w = rng.randint(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+  w = rng.randint(0, 2 ** 32, (n, 3), dtype=np.uint64).astype(np.uint32)
   fast, _ = _normals64(w)
   z = fast.reshape(-1)
   m = z.size
@@ -122,5 +128,10 @@ def test_bm64_normals_are_standard_normal():
   k4 = np.sum(np.abs(z) > 4)
   assert abs(k4 - m * p4) < 5 * np.sqrt(m * p4)
   assert scipy.stats.kstest(z[:1 << 21], 'norm').pvalue > 1e-3
-  # the two normals of a pair are uncorrelated
+  # the two normals of a pair are uncorrelated, and so are their squares
   assert abs(np.corrcoef(fast[:, 0], fast[:, 1])[0, 1]) < 5 / np.sqrt(n)
+  assert abs(np.corrcoef(fast[:, 0] ** 2, fast[:, 1] ** 2)[0, 1]) < 5 / np.sqrt(n)
+  # the angle is uniform over the full turn: equal mass in the 8 octants
+  oct_ = np.floor((np.arctan2(fast[:, 1], fast[:, 0]) + np.pi) / (np.pi / 4)).astype(int) % 8
+  cnt = np.bincount(oct_, minlength=8)
+  assert scipy.stats.chisquare(cnt).pvalue > 1e-3
