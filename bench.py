@@ -81,19 +81,45 @@ def _cpu_slice(args):
       return done, el
 
 
+def _cpu_mask():
+  """This process's CPU affinity as ranges ('0-255') and its count."""
+  cpus = sorted(os.sched_getaffinity(0))
+  rng, start = [], None
+  for i, c in enumerate(cpus):
+    if start is None:
+      start = c
+    if i + 1 == len(cpus) or cpus[i + 1] != c + 1:
+      rng.append(str(start) if start == c else '{}-{}'.format(start, c))
+      start = None
+  return ','.join(rng), len(cpus)
+
+
+def _cgroup_cpus():
+  """The cgroup CPU quota in CPUs (cpu.max), or None when unlimited."""
+  try:
+    quota, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+    return None if quota == 'max' else float(quota) / float(period)
+  except (OSError, ValueError):
+    return None
+
+
 def cpu_baseline(budget_s=6.0, chains=65536):
   """cfg2 on this host's cores, timed BEFORE the GPU is touched (the worker
   processes are forked from a process with no HIP state): the vectorised
   NumPy restatement (oracle/vector_mh.py, the reference's per-step arithmetic
   for all chains at once, every step recorded) at N = 65 536 on one core,
-  then split over P = min(16, cpu_count) processes (the box's CPU share).
-  The reference SP itself: 877 chain-steps/s on 1 core."""
+  then split over one process per CPU of the affinity mask (the
+  split across all host cores, mask stated).  The reference SP itself: 877
+  chain-steps/s on 1 core."""
   import multiprocessing as mp
   t = 16
   one_done, one_el = _cpu_slice((chains, t, budget_s, 1))
-  ncpu = os.cpu_count() or 1
-  procs = max(1, min(16, ncpu))
-  per = -(-chains // procs)
+  mask, ncpu = _cpu_mask()
+  quota = _cgroup_cpus()
+  procs = max(1, min(ncpu, 1000))   # the box allows 1024 processes
+  # independent chains per process; at least 4096 so that each process's
+  # vectorised steps stay efficient when the mask is wide
+  per = max(-(-chains // procs), 4096)
   ctx = mp.get_context('fork')
   with ctx.Pool(procs) as pool:
     res = pool.map(_cpu_slice, [(per, t, budget_s, 100 + i) for i in range(procs)])
@@ -101,14 +127,18 @@ def cpu_baseline(budget_s=6.0, chains=65536):
   return {'value': rate_all, 'unit': 'chain-steps/s', 'cores': procs,
           'kind': 'port',
           'single_core': one_done / one_el,
+          'affinity': mask, 'cgroup_cpu_quota': quota,
+          'reference_sp_1core': 877.0,
           'sample': 'cfg2 (d = 10), oracle/vector_mh.py vectorised NumPy '
                     'restatement, every step recorded: {} chains x {}-step '
                     'runs for {:.0f} s on 1 core ({:.3g} chain-steps/s), then '
-                    '{} processes x {} chains for {:.0f} s each (os.cpu_count '
-                    '= {}); the reference SP: 877 chain-steps/s on 1 core '
+                    '{} processes (one per CPU of the affinity mask {}; cgroup '
+                    'quota {} CPUs) x {} chains for {:.0f} s each; the '
+                    'reference SP: 877 chain-steps/s on 1 core '
                     '(BASELINE.md)'.format(chains, t, budget_s,
-                                           one_done / one_el, procs, per,
-                                           budget_s, ncpu)}
+                                           one_done / one_el, procs, mask,
+                                           quota if quota else 'unlimited',
+                                           per, budget_s)}
 
 
 def measured_traffic(chains, launch_steps, rng, trace):

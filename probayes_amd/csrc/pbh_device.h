@@ -418,6 +418,12 @@ __device__ __forceinline__ void st_buf16(void *base, uint32_t voff, uint16_t v) 
       __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b16(v, rs, (int)voff, 0, 0);
 }
+__device__ __forceinline__ void st_buf16(void *base, uint32_t voff, uint32_t soff,
+                                         uint16_t v) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b16(v, rs, (int)voff, (int)soff, 0);
+}
 
 // A pointer the compiler cannot prove wave-uniform but that is: its
 // first lane's value in SGPRs, so that a buffer resource built from it is
@@ -735,6 +741,25 @@ __device__ __forceinline__ Decision accept_filter_lead(double lpp, double lp,
   const bool af = fl <= __builtin_fmaf(eL, 0.999996f, -1.0f);
   const bool rf = fl > eL * 1.000004f;
   return Decision{inr && af, !(inr && (af || rf))};
+}
+
+// The same decision as lane masks (bit l = lane l; inactive lanes' bits are
+// meaningless): each comparison's ballot is the compare's own scalar result,
+// so acc / need combine in SALU instead of being turned into per-lane bools
+// and back (v_cndmask + v_cmp per ballot).  lin is wave-uniform.
+struct DecisionMask { uint64_t acc, need; };
+
+template <int LB>
+__device__ __forceinline__ DecisionMask accept_filter_lead_mask(double lpp, double lp,
+                                                                uint32_t lead, bool lin) {
+  const float eL = __builtin_amdgcn_exp2f(
+      (float)__builtin_fma(lpp - lp, 1.4426950408889634, (double)LB));
+  const float fl = (float)lead;
+  const uint64_t inr = lin ? 0ull : __ballot(__builtin_fabs(lpp) <= 700.) &
+                                        __ballot(__builtin_fabs(lp) <= 700.);
+  const uint64_t af = __ballot(fl <= __builtin_fmaf(eL, 0.999996f, -1.0f));
+  const uint64_t rf = __ballot(fl > eL * 1.000004f);
+  return DecisionMask{inr & af, ~(inr & (af | rf))};
 }
 
 // t = u01(t0, t1): the lead is t0's top 24 bits.

@@ -209,66 +209,105 @@ hipError_t launch_trace_expectation(const double *tx, const double *tlp,
 // autocorrelations of the centred series, the estimator of
 // scripts/bench_workloads.py ess_ips (rho_k = ac_k / ac_0 with ac_k =
 // sum_t xc_t xc_{t+k}; pairs rho_{2j+1} + rho_{2j+2} summed up to the first
-// non-positive one; ess = T / (1 + 2 sum)).  One thread per series (a wave's
-// 64 series are 512 contiguous bytes per record); autocovariances are formed
-// 32 lags per pass from a register window, passes stop at the first
-// non-positive pair.
+// non-positive one; ess = T / (1 + 2 sum)).
+// Layout: a QUAD of lanes per series (16 series per wave, contiguous chains
+// of one dim: each (lane j, t) load is a 128-byte row segment), lane j
+// taking the j-th quarter of the records; the quad's partial sums combine by
+// DPP (the same association in every lane, so the four lanes agree
+// bitwise).  The mean is one pass over the quarter; then passes of 32 lags
+// (K0 + 1 .. K0 + 32, lag 0 in the first): per record one load of x_t and
+// one of the lagged x_{t-K0-1} into a 32-entry register ring indexed by
+// t mod 32 (the record loop is unrolled by 32, so every ring index is
+// static) and 32 fp64 FMAs.  A wave stops after the pass in which all its
+// series reached a non-positive pair.
 constexpr int kEssLags = 32;
 
-__global__ void trace_ess_kernel(const double *tx, int64_t n, int32_t d,
-                                 int64_t first, int64_t T, double *ess) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t k = i / n, c = i % n;
-  if (k >= d) return;
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// sum over the quad, (a + b) + (c + d) in every lane
+__device__ __forceinline__ double quad_sum(double v) {
+  v = v + dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  return v + dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+}
+
+__global__ __launch_bounds__(256) void trace_ess_kernel(
+    const double *tx, int64_t n, int32_t d, int64_t first, int64_t T, double *ess) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = threadIdx.x & 3;
+  const int64_t sid = gid >> 2;              // series = k * n + c
+  const bool valid = sid < (int64_t)d * n;
+  const int64_t s0 = valid ? sid : 0;
+  const int64_t k = s0 / n, c = s0 % n;
   const int64_t stride = (int64_t)d * n;
   const double *xs = tx + (first * d + k) * n + c;
-  double mean = 0.;
-  for (int64_t t = 0; t < T; ++t) mean += xs[t * stride];
-  mean /= (double)T;
-  double ac0 = 0.;
-  for (int64_t t = 0; t < T; ++t) {
-    const double v = xs[t * stride] - mean;
-    ac0 = __builtin_fma(v, v, ac0);
-  }
-  const double inv0 = 1.0 / (ac0 > 1e-300 ? ac0 : 1e-300);
-  const int64_t m = (T - 1) / 2;   // pairs (lags 2j+1, 2j+2), j < m
-  double s = 0.;
-  bool done = m <= 0;
-  for (int64_t L0 = 1; !done; L0 += kEssLags) {   // lags L0 .. L0 + 31
-    double acc[kEssLags];
+  const int64_t seg = (T + 3) / 4;
+  const int64_t t0 = j * seg < T ? j * seg : T;
+  const int64_t t1 = t0 + seg < T ? t0 + seg : T;
+  double sum = 0.;
+  for (int64_t t = t0; t < t1; ++t) sum += xs[t * stride];
+  const double mean = quad_sum(sum) / (double)T;
+  const int64_t m = (T - 1) / 2;   // pairs (lags 2J+1, 2J+2), J < m
+  double ac0 = 0., inv0 = 0., s = 0.;
+  bool done = m <= 0 || !valid;
+  for (int64_t K0 = 0; __ballot(!done); K0 += kEssLags) {
+    // the ring R[(t - t0) mod 32] holds u_t = xc_{t-K0-1} (0 before record 0)
+    double R[kEssLags], acc[kEssLags];
 #pragma unroll
-    for (int l = 0; l < kEssLags; ++l) acc[l] = 0.;
-    for (int64_t t = 0; t + L0 < T; ++t) {
-      const double a = xs[t * stride] - mean;
+    for (int l = 0; l < kEssLags; ++l) {
+      acc[l] = 0.;
+      const int64_t tt = t0 - kEssLags + l - K0 - 1;   // u_{t0 - 32 + l}
+      R[l] = (l > 0 && tt >= 0 && tt < T) ? xs[tt * stride] - mean : 0.;
+    }
+    double a0 = 0.;
+    for (int64_t tb = t0; tb < t1; tb += kEssLags) {
 #pragma unroll
-      for (int l = 0; l < kEssLags; ++l) {
-        const int64_t u = t + L0 + l;
-        const double b = u < T ? xs[u * stride] - mean : 0.;
-        acc[l] = __builtin_fma(a, b, acc[l]);
+      for (int i = 0; i < kEssLags; ++i) {
+        const int64_t t = tb + i;
+        const bool in = t < t1;
+        const double xc = in ? xs[t * stride] - mean : 0.;
+        const int64_t tu = t - K0 - 1;
+        R[i] = (in && tu >= 0) ? xs[tu * stride] - mean : 0.;
+        if (K0 == 0) a0 = __builtin_fma(xc, xc, a0);
+#pragma unroll
+        for (int l = 0; l < kEssLags; ++l)
+          acc[l] = __builtin_fma(xc, R[(i - l + kEssLags) % kEssLags], acc[l]);
       }
     }
+    if (K0 == 0) {
+      ac0 = quad_sum(a0);
+      inv0 = 1.0 / (ac0 > 1e-300 ? ac0 : 1e-300);
+    }
 #pragma unroll
-    for (int l = 0; l < kEssLags; l += 2) {
-      const int64_t j = (L0 + l - 1) / 2;   // pair index of lags L0+l, L0+l+1
+    for (int l = 0; l < kEssLags; ++l) acc[l] = quad_sum(acc[l]);
+    // pairs (K0 + 2q + 1, K0 + 2q + 2) = acc[2q], acc[2q + 1]
+#pragma unroll
+    for (int q = 0; q < kEssLags / 2; ++q) {
       if (!done) {
-        if (j >= m) {
+        if (K0 / 2 + q >= m) {
           done = true;
         } else {
-          const double pr = acc[l] * inv0 + acc[l + 1] * inv0;
+          const double pr = acc[2 * q] * inv0 + acc[2 * q + 1] * inv0;
           if (pr <= 0.) done = true;
           else s += pr;
         }
       }
     }
   }
-  const double den = 1.0 + 2.0 * s;
-  ess[k * n + c] = (double)T / (den > 1e-12 ? den : 1e-12);
+  if (valid && j == 0) {
+    const double den = 1.0 + 2.0 * s;
+    ess[s0] = (double)T / (den > 1e-12 ? den : 1e-12);
+  }
 }
 
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
                             hipStream_t st) {
-  const int64_t m = (int64_t)d * n;
+  const int64_t m = 4 * (int64_t)d * n;   // a quad of lanes per series
   hipLaunchKernelGGL(trace_ess_kernel, dim3((unsigned)((m + 255) / 256)),
                      dim3(256), 0, st, tx, n, d, first, count, ess);
   return hipGetLastError();

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "../../include/pbhip.h"
@@ -68,7 +69,7 @@ struct pbh_engine {
   // production fp64 normal tables (bm64, pbh_device.h), read into LDS
   double *bm64 = nullptr;
   double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
-  bool spin_sync = true;     // PBH_SYNC=block: hipStreamSynchronize instead
+  bool spin_sync = true;     // poll <= 2 ms, then block; PBH_SYNC=block: block
   // timing events as marker packets around the launches (default), or
   // PBH_EVENT_MARKERS=0: on the first / last dispatch packet
   // (hipExtLaunchKernel: 2 us less GPU time, 3-4 us more host enqueue and
@@ -959,10 +960,17 @@ int pbh_sync(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   HIP_TRY(hipSetDevice(e->device));
   if (e->spin_sync) {
-    // poll the stream: returns within a microsecond or so of the last
-    // kernel's completion (a blocking wait sleeps on the completion signal)
+    // poll the stream for up to 2 ms: a short launch's completion is seen
+    // within a microsecond or so (a blocking wait sleeps on the completion
+    // signal and wakes ~10 us late); longer waits block, so that a long run
+    // does not hold a host core at 100 %
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t q;
     while ((q = hipStreamQuery(e->stream)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
+        q = hipStreamSynchronize(e->stream);
+        break;
+      }
     }
     HIP_TRY(q);
   } else {
@@ -1290,64 +1298,99 @@ int pbh_rccl_init(pbh_engine *e, int32_t rank, int32_t world, const uint8_t id[1
 namespace {
 
 // Every rank enters every collective of a gather, whatever failed locally: a
-// rank that cannot proceed contributes NaN to an all-reduce of (status,
-// count) and every rank then returns the same error -- no rank is left
-// waiting inside RCCL (a collective only some ranks enter never completes).
+// rank that cannot proceed votes NaN in an all-reduce of (status, count) and
+// every rank then returns the same error -- no rank is left waiting inside
+// RCCL (a collective only some ranks enter never completes).  Local HIP
+// failures between two agreements are not returned on the spot: they become
+// the rank's vote at the next agreement, which every rank enters.
 int rccl_agree(pbh_engine *e, bool ok, int64_t n, int64_t *n_max, const char *what) {
   double v[3] = {ok ? 0. : std::nan(""), (double)n, -(double)n};
-  HIP_TRY(hipMemcpy(e->scalar, v, sizeof v, hipMemcpyHostToDevice));
-  RCCL_TRY(ncclAllReduce(e->scalar, e->scalar, 3, ncclFloat64, ncclMax, e->comm,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(v, e->scalar, sizeof v, hipMemcpyDeviceToHost));
+  hipError_t h = hipMemcpy(e->scalar, v, sizeof v, hipMemcpyHostToDevice);
+  if (h != hipSuccess)   // the vote must still say "failed": all-ones is a NaN
+    (void)hipMemset(e->scalar, 0xFF, sizeof(double));
+  // the collective is entered whatever happened above
+  const ncclResult_t r = ncclAllReduce(e->scalar, e->scalar, 3, ncclFloat64, ncclMax,
+                                       e->comm, e->stream);
+  hipError_t s = hipStreamSynchronize(e->stream);
+  if (s == hipSuccess) s = hipMemcpy(v, e->scalar, sizeof v, hipMemcpyDeviceToHost);
+  if (r != ncclSuccess)
+    return fail(PBH_ERR_RCCL, "%s: %s", what, ncclGetErrorString(r));
+  if (h != hipSuccess || s != hipSuccess)
+    return fail(PBH_ERR_HIP, "%s: %s", what, hipGetErrorString(h != hipSuccess ? h : s));
   if (v[0] != v[0])
     return fail(PBH_ERR_STATE, "%s: a rank could not take part (see its own error)", what);
   if (n_max) *n_max = (int64_t)v[1];
   return PBH_OK;
 }
 
+// Fault injection for the tests (PBH_FAULT_GATHER="rank[:step]", step 1 =
+// no chains, 2 = the buffers, 3 = packing; default 3): this rank fails that
+// step of pbh_rccl_allgather_stats locally.
+bool fault_at(const pbh_engine *e, int step) {
+  const char *f = std::getenv("PBH_FAULT_GATHER");
+  if (!f || !*f) return false;
+  int rank = -1, st = 3;
+  if (std::sscanf(f, "%d:%d", &rank, &st) < 1) return false;
+  return rank == e->rank && st == step;
+}
+
+hipError_t keep(hipError_t acc, hipError_t e) { return acc != hipSuccess ? acc : e; }
+
 }  // namespace
 
 int pbh_rccl_max_chains(pbh_engine *e, int64_t *n_max) {
   if (check_ptr(e, "engine") || check_ptr(n_max, "n_max")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
-  HIP_TRY(hipSetDevice(e->device));
-  return rccl_agree(e, e->x != nullptr, e->n, n_max, "pbh_rccl_max_chains");
+  const bool ok = hipSetDevice(e->device) == hipSuccess;
+  return rccl_agree(e, ok && e->x != nullptr, e->n, n_max, "pbh_rccl_max_chains");
 }
 
 int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
-  if (check_ptr(e, "engine") || check_ptr(out, "out") || check_ptr(counts, "counts"))
-    return PBH_ERR_ARG;
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
-  HIP_TRY(hipSetDevice(e->device));
+  // a bad argument is this rank's failure: it still takes part
+  bool ok = out != nullptr && counts != nullptr;
+  ok = hipSetDevice(e->device) == hipSuccess && ok;
   // 1. agree on the padded width; a rank without chains stops everyone
   int64_t nm = 0;
-  int rc = rccl_agree(e, e->x != nullptr, e->n, &nm, "pbh_rccl_allgather_stats");
+  int rc = rccl_agree(e, ok && e->x != nullptr && !fault_at(e, 1), e->n, &nm,
+                      "pbh_rccl_allgather_stats");
   if (rc) return rc;
   const int64_t n = e->n, d = e->d, rows = 3 * d + 2;   // + the count row
-  // 2. buffers (a failure is reported through the next agreement)
-  const bool ok = !dalloc(e->gather_send, (size_t)rows * nm) &&
-                  !dalloc(e->gather_recv, (size_t)rows * nm * e->world);
+  // 2. buffers
+  ok = !dalloc(e->gather_send, (size_t)rows * nm) &&
+       !dalloc(e->gather_recv, (size_t)rows * nm * e->world) && !fault_at(e, 2);
   rc = rccl_agree(e, ok, n, nullptr, "pbh_rccl_allgather_stats (buffers)");
   if (rc) return rc;
-  // 3. pack [rows][nm]: sum, sumsq, n_acc, ess, then the rank's count
-  HIP_TRY(hipMemsetAsync(e->gather_send, 0, (size_t)rows * nm * sizeof(double), e->stream));
+  // 3. pack [rows][nm]: sum, sumsq, n_acc, ess, then the rank's count; a
+  // failure here is this rank's vote at the third agreement
+  hipError_t err = hipMemsetAsync(e->gather_send, 0, (size_t)rows * nm * sizeof(double),
+                                  e->stream);
   const size_t pitch = (size_t)nm * sizeof(double);
-  HIP_TRY(hipMemcpy2DAsync(e->gather_send, pitch, e->msum, n * sizeof(double),
-                           n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
-  HIP_TRY(hipMemcpy2DAsync(e->gather_send + d * nm, pitch, e->msq, n * sizeof(double),
-                           n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
-  hipLaunchKernelGGL(nacc_to_f64, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                     0, e->stream, e->nacc, e->gather_send + 2 * d * nm, n);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpy2DAsync(e->gather_send + (2 * d + 1) * nm, pitch, e->ess,
-                           n * sizeof(double), n * sizeof(double), d,
-                           hipMemcpyDeviceToDevice, e->stream));
+  err = keep(err, hipMemcpy2DAsync(e->gather_send, pitch, e->msum, n * sizeof(double),
+                                   n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
+  err = keep(err, hipMemcpy2DAsync(e->gather_send + d * nm, pitch, e->msq, n * sizeof(double),
+                                   n * sizeof(double), d, hipMemcpyDeviceToDevice, e->stream));
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL(nacc_to_f64, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                       0, e->stream, e->nacc, e->gather_send + 2 * d * nm, n);
+    err = hipGetLastError();
+  }
+  err = keep(err, hipMemcpy2DAsync(e->gather_send + (2 * d + 1) * nm, pitch, e->ess,
+                                   n * sizeof(double), n * sizeof(double), d,
+                                   hipMemcpyDeviceToDevice, e->stream));
   const double cnt = (double)n;
-  HIP_TRY(hipMemcpyAsync(e->gather_send + (3 * d + 1) * nm, &cnt, sizeof cnt,
-                         hipMemcpyHostToDevice, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  // 4. the one all-gather over xGMI
+  err = keep(err, hipMemcpyAsync(e->gather_send + (3 * d + 1) * nm, &cnt, sizeof cnt,
+                                 hipMemcpyHostToDevice, e->stream));
+  err = keep(err, hipStreamSynchronize(e->stream));
+  rc = rccl_agree(e, err == hipSuccess && !fault_at(e, 3), n, nullptr,
+                  "pbh_rccl_allgather_stats (packing)");
+  if (rc) {
+    if (err != hipSuccess)
+      return fail(PBH_ERR_HIP, "pbh_rccl_allgather_stats: %s", hipGetErrorString(err));
+    return rc;
+  }
+  // 4. the one all-gather over xGMI (every rank is here)
   RCCL_TRY(ncclAllGather(e->gather_send, e->gather_recv, (size_t)rows * nm,
                          ncclFloat64, e->comm, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1365,12 +1408,22 @@ int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
 int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
   if (check_ptr(e, "engine") || check_ptr(value, "value")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
-  HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(hipMemcpy(e->scalar, value, sizeof(double), hipMemcpyHostToDevice));
-  RCCL_TRY(ncclAllReduce(e->scalar, e->scalar, 1, ncclFloat64, ncclMax, e->comm,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(value, e->scalar, sizeof(double), hipMemcpyDeviceToHost));
+  double v = *value;
+  hipError_t h = hipSetDevice(e->device);
+  h = keep(h, hipMemcpy(e->scalar, &v, sizeof(double), hipMemcpyHostToDevice));
+  if (h != hipSuccess) (void)hipMemset(e->scalar, 0xFF, sizeof(double));   // NaN: failed
+  // entered whatever happened above (a NaN max tells every rank)
+  const ncclResult_t r = ncclAllReduce(e->scalar, e->scalar, 1, ncclFloat64, ncclMax,
+                                       e->comm, e->stream);
+  hipError_t s = hipStreamSynchronize(e->stream);
+  if (s == hipSuccess) s = hipMemcpy(&v, e->scalar, sizeof(double), hipMemcpyDeviceToHost);
+  if (r != ncclSuccess) return fail(PBH_ERR_RCCL, "pbh_rccl_allreduce_max: %s",
+                                    ncclGetErrorString(r));
+  if (h != hipSuccess || s != hipSuccess)
+    return fail(PBH_ERR_HIP, "pbh_rccl_allreduce_max: %s",
+                hipGetErrorString(h != hipSuccess ? h : s));
+  if (v != v) return fail(PBH_ERR_STATE, "pbh_rccl_allreduce_max: a rank failed");
+  *value = v;
   return PBH_OK;
 }
 

@@ -1069,20 +1069,23 @@ void mh_pair_kernel(KArgs a) {
     // half 1 holds the full density and the threshold: its decision is the
     // chain's (computed branch-free in both halves; half 0's is discarded)
     const bool first = !a.has_pred && s == 0;   // s = None on step 1
-    bool acc;
+    constexpr uint64_t kHi = 0xFFFFFFFF00000000ull;
+    uint64_t accm;   // lane mask of the decisions (half 1's bits count)
     double eA = 0.;
     if (REPLAY) {
       eA = lin ? lpp : exp_logp(lpp, a.log_npi);
       double q = eA / np_max_tiny(eB);
       q = q < 1. ? q : 1.;
-      acc = first || q >= thr;
+      accm = __ballot(first || q >= thr);
     } else {
-      const Decision dc = PHX ? accept_filter_lead<PD::LB>(lpp, lp, t0, lin)
-                              : accept_filter(lpp, lp, t0, lin);
-      acc = first || dc.acc;
-      // half 1's undecided lanes (scalar mask ops; first is wave-uniform)
-      const uint64_t needm = first ? 0ull : __ballot(dc.need) & 0xFFFFFFFF00000000ull;
+      // masks straight from the comparisons (no per-lane bool round trip)
+      const DecisionMask dm = accept_filter_lead_mask<PHX ? PD::LB : 24>(
+          lpp, lp, PHX ? t0 : t0 >> 8, lin);
+      accm = first ? ~0ull : dm.acc;
+      // half 1's undecided lanes (first is wave-uniform)
+      const uint64_t needm = first ? 0ull : dm.need & kHi & __ballot(true);
       if (needm) {   // wave-uniform, rare
+        bool ex = false;
         if (__builtin_amdgcn_inverse_ballot_w64(needm)) {
           double t;
           if (PHX) {
@@ -1093,13 +1096,14 @@ void mh_pair_kernel(KArgs a) {
           } else {
             t = u01(t0, t1);
           }
-          acc = ratio_accept(lpp, lp, t, lin, a.log_npi);
+          ex = ratio_accept(lpp, lp, t, lin, a.log_npi);
         }
+        accm = (accm & ~needm) | (__ballot(ex) & needm);
       }
     }
     // half 1's decision is the chain's: lanes l and l + 32 both take bit
-    // l + 32 of the ballot (SGPR mask ops; inverse_ballot feeds v_cndmask)
-    const uint64_t mhi = __ballot(hi && acc) & 0xFFFFFFFF00000000ull;
+    // l + 32 of the mask (SGPR mask ops; inverse_ballot feeds v_cndmask)
+    const uint64_t mhi = accm & kHi;
     const uint64_t macc = mhi | (mhi >> 32);   // lane mask of the chain's decision
     const bool accl = __builtin_amdgcn_inverse_ballot_w64(macc);
 #pragma unroll
@@ -1532,6 +1536,20 @@ __device__ __forceinline__ Decision accept_filter_rel32(float sp, float ls32, bo
   return Decision{(bool)(inr & af), !(inr & (af | rf))};
 }
 
+// The same as lane masks (accept_filter_lead_mask): inrm is the ballot of
+// the range condition.
+template <int LB>
+__device__ __forceinline__ DecisionMask accept_filter_rel32_mask(float sp, float ls32,
+                                                                 uint64_t inrm,
+                                                                 uint32_t lead) {
+  constexpr float w = 1.0f / (float)(1u << LB);
+  const float tlo = (float)lead * w;
+  const float thi = tlo + w;
+  const uint64_t af = __ballot(thi * ls32 <= sp * 0.999996f);
+  const uint64_t rf = __ballot(tlo * ls32 > sp * 1.000004f);
+  return DecisionMask{inrm & af, ~(inrm & (af | rf))};
+}
+
 __device__ __forceinline__ double max_f64_raw(double a, double b) {
   double r;
   asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -1614,6 +1632,11 @@ void mh_gmm_quad_kernel(KArgs a) {
     const uint32_t lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
     double gm[4], gs[4];     // the group's states (M, S), for the records
     int64_t grec[4];
+    // FULL: the group's record rows as scalar buffer bases, one pair of
+    // readfirstlanes per group (step j stores at byte offset j * row bytes)
+    double *const gtx = FULL ? wave_uniform(txrow) : nullptr;
+    uint16_t *const gacc = FULL ? wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W))
+                                : nullptr;
     // one step of the group; j is a compile-time constant (DPP controls)
     auto step = [&](auto J) {
       constexpr int j = decltype(J)::value;
@@ -1654,12 +1677,20 @@ void mh_gmm_quad_kernel(KArgs a) {
       e = e + qperm_f64<kQuadXor1>(e);
       const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
       bool acc;
+      uint64_t accm = 0;   // FULL: the decisions as a lane mask
       if constexpr (FULL) {
-        const Decision dc = accept_filter_rel32<LB>(E32, ls32, inr, lead);
-        acc = dc.acc;
-        if (__ballot(dc.need)) {   // wave-uniform, rare
-          if (dc.need) acc = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
+        const uint64_t inrm = __ballot(__builtin_fabs(M) <= 698.) &
+                              __ballot(__builtin_fabs(lm) <= 698.);
+        const DecisionMask dm = accept_filter_rel32_mask<LB>(E32, ls32, inrm, lead);
+        accm = dm.acc;
+        const uint64_t needm = dm.need & __ballot(true);
+        if (needm) {   // wave-uniform, rare
+          bool ex = false;
+          if (__builtin_amdgcn_inverse_ballot_w64(needm))
+            ex = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
+          accm = (accm & ~needm) | (__ballot(ex) & needm);
         }
+        acc = __builtin_amdgcn_inverse_ballot_w64(accm);
       } else if (!a.has_pred && s == 0) {
         acc = true;                                  // s = None on step 1
       } else {
@@ -1679,11 +1710,19 @@ void mh_gmm_quad_kernel(KArgs a) {
           }
         }
       }
+      if constexpr (FULL) {   // selects on the mask (no bool round trip)
 #pragma unroll
-      for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
-      lm = acc ? M : lm;
-      ls = acc ? S : ls;
-      ls32 = acc ? (float)S : ls32;
+        for (int i = 0; i < D; ++i) x[i] = sel_f64(accm, x[i], xp[i]);
+        lm = sel_f64(accm, lm, M);
+        ls = sel_f64(accm, ls, S);
+        ls32 = sel_f32(accm, ls32, (float)S);
+      } else {
+#pragma unroll
+        for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
+        lm = acc ? M : lm;
+        ls = acc ? S : ls;
+        ls32 = acc ? (float)S : ls32;
+      }
       gm[j] = lm;
       gs[j] = ls;
       if constexpr (MOM) {
@@ -1700,15 +1739,15 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int i = 1; i < D; ++i) xo = p % D == i ? x[i] : xo;
         // the record row is wave-uniform: a scalar buffer resource (without
         // readfirstlane the compiler wraps the store in a waterfall loop)
-        st_buf(wave_uniform(txrow), xoff, 0, xo);
+        st_buf(gtx, xoff, (uint32_t)(j * rstride * 8), xo);
         grec[j] = ri;
-        uint64_t m = __ballot(acc) & 0x1111111111111111ull & act_bits;
+        uint64_t m = accm & 0x1111111111111111ull & act_bits;
         m = (m | (m >> 3)) & 0x0303030303030303ull;
         m = (m | (m >> 6)) & 0x000F000F000F000Full;
         m = (m | (m >> 12)) & 0x000000FF000000FFull;
         m = (m | (m >> 24)) & 0xFFFFull;
         // every lane stores the wave's word (one address, one value)
-        st_buf16(wave_uniform(a.tacc + ri * a.W), (uint32_t)(wave * 2), (uint16_t)m);
+        st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), (uint16_t)m);
         ++ri;
         txrow += rstride;
         return;
@@ -2412,6 +2451,7 @@ inline bool gmm_pair_form(const KArgs &a) {
 // acc_beta = 1.  PBH_GMM_FULL=0 (engine: gmm_full) keeps the general form.
 inline bool gmm_quad_full(const KArgs &a) {
   return a.gmm_full && a.has_pred && a.acc_beta == 1.0 && a.thin == 1 &&
+         (int64_t)4 * a.d * a.n * 8 < (int64_t(1) << 32) &&   // group row offsets
          a.tx != nullptr && a.g0 % 4 == 0 && a.n_steps % 4 == 0 &&
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }

@@ -15,6 +15,7 @@ engine's RCCL calls in CPU tests of the rank logic (tests/test_dist.py) and
 packs blocks exactly like the engine (pack_stats / engine.unpack_stats).
 """
 import io
+import os
 import socket
 import struct
 import time
@@ -79,6 +80,20 @@ def _connect(addr, port, timeout):
       time.sleep(0.05)
 
 
+class CollectiveError(RuntimeError):
+  """A rank failed inside a collective; every rank raises it."""
+
+
+def fault_at(rank, step):
+  """PBH_FAULT_GATHER='rank[:step]' (step 1 chains, 2 buffers, 3 packing;
+  default 3): the engine's fault injection, read the same way here."""
+  f = os.environ.get('PBH_FAULT_GATHER', '')
+  if not f:
+    return False
+  r, _, st = f.partition(':')
+  return int(r) == rank and int(st or 3) == step
+
+
 class TcpCollective:
   """Star-topology exchange over TCP: rank 0 listens on (addr, port), the
   other ranks connect and announce their rank.  Used for the ncclUniqueId
@@ -101,6 +116,17 @@ class TcpCollective:
           conn, _ = srv.accept()
           conn.settimeout(timeout)
           (r,) = struct.unpack('<i', _recv_exact(conn, 4))
+          if not 1 <= r < self.world or r in self.peers:
+            # a stale process on the port, or a misconfigured launch: fail
+            # now rather than time out or lose a rank's contribution
+            conn.close()
+            for c in self.peers.values():
+              c.close()
+            raise ConnectionError(
+                'rank 0 got a connection announcing rank {} ({}; world {}, '
+                'ranks connected: {})'.format(
+                    r, 'already connected' if r in self.peers else 'out of range',
+                    self.world, sorted(self.peers)))
           self.peers[r] = conn
       finally:
         srv.close()
@@ -146,12 +172,29 @@ class TcpCollective:
   def allreduce_max(self, value):
     return float(self.allgather(np.array([float(value)])).max())
 
+  def agree(self, ok, n, what):
+    """pbh_engine's rccl_agree: every rank votes (status, count); a rank
+    that failed locally votes NaN and every rank raises the same error."""
+    v = self.allgather(np.array([0. if ok else np.nan, float(n)]))
+    if np.isnan(v[:, 0]).any():
+      raise CollectiveError('{}: rank(s) {} could not take part'.format(
+          what, [int(r) for r in np.flatnonzero(np.isnan(v[:, 0]))]))
+    return v[:, 1].astype(np.int64)
+
   def allgather_stats(self, sum_, sumsq, n_acc, ess=None):
     """The engine's pbh_rccl_allgather_stats contract on the CPU: the
-    padded [world][3d+1][n_max] block and every rank's count."""
+    padded [world][3d+1][n_max] block and every rank's count, behind the same
+    agreements (chains, buffers, packing; PBH_FAULT_GATHER injects a local
+    failure) so that a failing rank makes every rank fail, none wait."""
     n = np.asarray(sum_).shape[0]
-    counts = self.allgather(np.array([n], np.int64))[:, 0]
-    blk = pack_stats(sum_, sumsq, n_acc, ess, n_max=int(counts.max()))
+    counts = self.agree(not fault_at(self.rank, 1), n, 'allgather_stats')
+    self.agree(not fault_at(self.rank, 2), n, 'allgather_stats (buffers)')
+    ok = not fault_at(self.rank, 3)
+    try:
+      blk = pack_stats(sum_, sumsq, n_acc, ess, n_max=int(counts.max()))
+    except Exception:   # this rank's failure is its vote
+      ok, blk = False, None
+    self.agree(ok, n, 'allgather_stats (packing)')
     return self.allgather(blk), counts
 
   def close(self):

@@ -188,3 +188,72 @@ def test_unique_id_handoff_and_ragged_gather_three_ranks(tmp_path):
   script.write_text(UID_WORKER.format(root=ROOT))
   outs = _spawn(script, 3, _free_port())
   assert all('UID_OK' in o for o in outs), outs
+
+
+def test_rank0_rejects_a_duplicate_or_out_of_range_rank():
+  """a stale process on the port announcing a rank already
+  connected (or one outside 1..world-1) makes rank 0 fail at once."""
+  import struct
+  import threading
+  from probayes_amd.dist import TcpCollective
+  for bad in (1, 5):
+    port = _free_port()
+    err = []
+
+    def rank0():
+      try:
+        TcpCollective(0, 3, '127.0.0.1', port, timeout=20)
+      except ConnectionError as e:
+        err.append(str(e))
+
+    t = threading.Thread(target=rank0)
+    t.start()
+    socks = []
+    for r in ((1, bad) if bad == 1 else (bad,)):
+      for _ in range(200):
+        try:
+          s = socket.create_connection(('127.0.0.1', port), timeout=5)
+          break
+        except OSError:
+          import time
+          time.sleep(0.02)
+      s.sendall(struct.pack('<i', r))
+      socks.append(s)
+    t.join(30)
+    assert not t.is_alive()
+    assert err and ('already connected' in err[0] or 'out of range' in err[0]), err
+    for s in socks:
+      s.close()
+
+
+FAULT_WORKER = r'''
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from probayes_amd.dist import TcpCollective, CollectiveError, shard
+rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+col = TcpCollective(rank, world, '127.0.0.1', int(os.environ['MASTER_PORT']), timeout=30)
+off, n = shard(9, rank, world)
+s = np.ones((n, 2))
+try:
+  col.allgather_stats(s, s, np.zeros(n))
+  print('NO_ERROR', rank)
+except CollectiveError as e:
+  assert '[1]' in str(e), str(e)
+  # the protocol stays in step after a failure: the next collective works
+  assert col.allreduce_max(rank) == world - 1
+  print('FAILED_AS_ONE', rank)
+col.close()
+'''
+
+
+@pytest.mark.parametrize('step', ['1', '2', '3'])
+def test_a_rank_failing_inside_the_gather_fails_every_rank(tmp_path, monkeypatch, step):
+  """Rank 1 fails locally at step `step` of the stats gather
+  (PBH_FAULT_GATHER=1:step, the engine's fault injection): rank 0 fails with
+  it instead of waiting in the all-gather, and both stay usable."""
+  monkeypatch.setenv('PBH_FAULT_GATHER', '1:' + step)
+  script = tmp_path / 'fault.py'
+  script.write_text(FAULT_WORKER.format(root=ROOT))
+  outs = _spawn(script, 2, _free_port())
+  assert 'FAILED_AS_ONE 0' in outs[0] and 'FAILED_AS_ONE 1' in outs[1], outs

@@ -216,6 +216,30 @@ def test_rccl_single_rank_allgather_and_max():
   eng.close()
 
 
+@pytest.mark.parametrize('step', ['1', '2', '3'])
+def test_rccl_gather_local_failure_is_returned_after_the_collectives(monkeypatch, step):
+  """PBH_FAULT_GATHER=0:step makes this rank fail step `step` of
+  pbh_rccl_allgather_stats locally: the call still enters every agreement
+  (so no peer would wait) and returns the error; the engine and its
+  communicator stay usable."""
+  from probayes_amd import Engine
+  from probayes_amd._lib import PbhError
+  eng = Engine(_diag10_spec())
+  eng.init_chains(np.zeros((300, 10)))
+  eng.set_rng('philox', 3)
+  eng.alloc_trace(8, 1)
+  eng.run(8)
+  eng.rccl_init(0, 1, Engine.rccl_unique_id())
+  monkeypatch.setenv('PBH_FAULT_GATHER', '0:' + step)
+  with pytest.raises(PbhError, match='could not take part'):
+    eng.rccl_allgather_stats()
+  monkeypatch.delenv('PBH_FAULT_GATHER')
+  g = eng.rccl_allgather_stats()
+  assert list(g['counts']) == [300]
+  assert eng.rccl_allreduce_max(1.5) == 1.5
+  eng.close()
+
+
 def _ess_ips(x):
   """scripts/bench_workloads.py's host estimator (FFT autocorrelation)."""
   n, t = x.shape
@@ -350,26 +374,35 @@ def test_iid_normal_pairwise_tree_matches_numpy(n_obs):
 @pytest.mark.parametrize('name', ['metrohast_norm1d', 'gmm2'])
 def test_production_modes_agree_with_reference_arithmetic(name):
   """Production Philox (fast densities, filtered acceptance incl. the
-  e-tempered tuple-tran form of App. A-1) against PHILOX_F64 (fp64
-  Box-Muller, the reference's arithmetic): the same posterior within
-  Monte-Carlo error."""
+  e-tempered tuple-tran form of App. A-1) against PHILOX_F64 (libm fp64
+  Box-Muller, the reference's arithmetic): the same law.  Both runs start
+  from the same init, so every step's expectation is the same under the
+  same law; the chains are independent, so the Monte-Carlo standard error of
+  a post-burn-in average is the sd of the per-chain averages / sqrt(N) (it
+  carries each chain's autocorrelation).  Means, second moments and the
+  accept rate agree within 5 combined MCSE."""
   spec = oracle.golden_spec(name)
   n, t, burn = 4096, 800, 300
   res = {}
   for mode in ('philox', 'philox_f64'):
     eng = _engine(spec)
     eng.init_chains(golden_init(name, n))
-    eng.set_rng(mode, seed=77)
+    eng.set_rng(mode, seed=77 if mode == 'philox' else 78)
     eng.alloc_trace(t, 1)
     eng.run(t)
     tr = eng.trace()
     eng.close()
-    v = tr['v_x'][:, burn:]
-    res[mode] = (v.mean(axis=(0, 1)), v.std(axis=(0, 1)), tr['u'].mean())
-  (m1, s1, a1), (m0, s0, a0) = res['philox'], res['philox_f64']
-  assert np.all(np.abs(m1 - m0) < 0.05 * s0), (m1, m0, s0)
-  assert np.all(np.abs(s1 / s0 - 1) < 0.05), (s1, s0)
-  assert abs(a1 - a0) < 0.02, (a1, a0)
+    v = tr['v_x'][:, burn:]                       # [N, T', d]
+    per = {'mean': v.mean(axis=1), 'sq': (v * v).mean(axis=1),
+           'acc': tr['u'][:, burn:].mean(axis=1)[:, None]}
+    res[mode] = {k: (a.mean(axis=0), a.std(axis=0, ddof=1) / np.sqrt(n))
+                 for k, a in per.items()}
+  for k in ('mean', 'sq', 'acc'):
+    (m1, e1), (m0, e0) = res['philox'][k], res['philox_f64'][k]
+    z = np.abs(m1 - m0) / np.sqrt(e1 ** 2 + e0 ** 2)
+    assert np.all(z < 5), (name, k, m1, m0, z)
+    assert np.all(np.maximum(e1, e0) < 0.05 * np.maximum(np.abs(m0), 0.1)), \
+        (name, k, e1, e0)   # the band is tight enough to mean something
 
 
 @pytest.mark.parametrize('lanes', ['2', '4'])
