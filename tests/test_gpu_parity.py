@@ -393,16 +393,20 @@ def test_production_modes_agree_with_reference_arithmetic(name):
     tr = eng.trace()
     eng.close()
     v = tr['v_x'][:, burn:]                       # [N, T', d]
-    per = {'mean': v.mean(axis=1), 'sq': (v * v).mean(axis=1),
-           'acc': tr['u'][:, burn:].mean(axis=1)[:, None]}
-    res[mode] = {k: (a.mean(axis=0), a.std(axis=0, ddof=1) / np.sqrt(n))
-                 for k, a in per.items()}
+    u = tr['u'][:, burn:].astype(np.float64)[..., None]
+    draws = {'mean': v, 'sq': v * v, 'acc': u}   # [N, T', d] per statistic
+    res[mode] = {k: (a.mean(axis=1).mean(axis=0),
+                     a.mean(axis=1).std(axis=0, ddof=1) / np.sqrt(n),
+                     a.reshape(-1, a.shape[-1]).std(axis=0))
+                 for k, a in draws.items()}
   for k in ('mean', 'sq', 'acc'):
-    (m1, e1), (m0, e0) = res['philox'][k], res['philox_f64'][k]
+    (m1, e1, _), (m0, e0, sd) = res['philox'][k], res['philox_f64'][k]
     z = np.abs(m1 - m0) / np.sqrt(e1 ** 2 + e0 ** 2)
     assert np.all(z < 5), (name, k, m1, m0, z)
-    assert np.all(np.maximum(e1, e0) < 0.05 * np.maximum(np.abs(m0), 0.1)), \
-        (name, k, e1, e0)   # the band is tight enough to mean something
+    # the band is tight enough to mean something: the MCSE is under 5 % of
+    # the statistic's own spread over the draws (a multimodal target's
+    # coordinate mean can sit near 0, so |mean| is no scale)
+    assert np.all(np.maximum(e1, e0) < 0.05 * sd), (name, k, e1, e0, sd)
 
 
 @pytest.mark.parametrize('lanes', ['2', '4'])

@@ -121,12 +121,15 @@ def test_caller_draws_between_steps_are_seen_as_the_reference_sees_them():
   rs = np.random.RandomState(seed)
   streams = np.empty((T, oracle.stream_width(spec), 1))
   user = []
+  kind = spec['proposal']['kind']
+  assert kind in ('gauss', 'sphere')   # metrohast_norm1d: the tuple delta
   for s in range(T):
-    streams[s, :-1, 0] = rs.standard_normal(spec['dim'])
+    # oracle/streams.py's per-step order: the proposal's draws, then t
+    streams[s, :-1, 0] = (rs.standard_normal(spec['dim']) if kind == 'gauss'
+                          else rs.random_sample(spec['dim']))
     streams[s, -1, 0] = rs.random_sample()
     if s % 5 == 2:
       user.append(rs.random_sample())
-  assert spec['proposal']['kind'] == 'gauss'
   ref = oracle.run_mh(spec, golden_init(name, 1), streams)
   np.random.seed(seed)
   sm = process.sampler(*args, chunk=64, **kwds)
