@@ -45,6 +45,40 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0,
   return c;
 }
 
+// The ten round keys in VGPRs (uniform values kept out of the SGPR file:
+// the steady-state loops run short of SGPRs, and a uniform value the
+// compiler demotes on its own costs a readfirstlane loop per buffer store).
+// The v_mov is an asm so that the result counts as divergent.
+struct PhiloxKeys { uint32_t k0[10], k1[10]; };
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t v) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(v));
+  return r;
+}
+__device__ __forceinline__ PhiloxKeys philox_keys_v(uint32_t k0, uint32_t k1) {
+  PhiloxKeys k;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    k.k0[i] = in_vgpr(k0 + (uint32_t)i * 0x9E3779B9u);
+    k.k1[i] = in_vgpr(k1 + (uint32_t)i * 0xBB67AE85u);
+  }
+  return k;
+}
+// philox4x32_10 on precomputed round keys (the same bijection)
+__device__ __forceinline__ u32x4 philox4x32_10_rk(u32x4 c, const PhiloxKeys &k) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)M0 * c.x;
+    const uint64_t p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k.k0[i], 0x96), lo1,
+              (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k.k1[i], 0x96), lo0};
+  }
+  return c;
+}
+
 // xoshiro128** (Blackman & Vigna 2018): 128-bit state, 32-bit outputs,
 // passes BigCrush; ~10 full-rate integer ops per word against ~55 mixed-rate
 // ops per 4 words of Philox-4x32-10 (20 of them v_mad_u64_u32).  One
@@ -235,7 +269,7 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 //             |r| <= 2^-11, q(r) = -2 log1p(r) / r to degree 4 (truncation
 //             r^5 / 6 < 2^-58 relative); u1 -> 1 takes c = 1 and T = 0, so E
 //             keeps its relative accuracy there;
-//   sqrt    = v_rsq_f64 + two Newton steps;
+//   sqrt    = v_rsq_f64 + one third-order (Goldschmidt) correction;
 //   (sin, cos)(alpha) = table angle J rotated by theta < pi/512: sin degree
 //             5, cos degree 4 (truncations 2e-19 relative, 1e-18 absolute).
 // The bit positions make every index one VALU op: the hi word of 1 + k1
@@ -243,15 +277,18 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 // b & 0xFFC (the table is four arrays of 32-bit words: sin lo, sin hi, cos
 // lo, cos hi), the log row's byte offset is a v_bfe of c_j's hi word.
 // Tables (host-computed in long double, pbh_dispatch.cpp bm64_tables) live
-// in LDS: 1025 {-2 ln c_j, 1/c_j} pairs and 1024 {sin, cos} values (the full
-// turn, exact quadrant symmetry), 33 KB with the exp2 table.  About 38 VALU
-// per pair.  A 128-bit Philox block carries one pair and a 32-bit word
+// in LDS: 1024 {sin, cos} values (the full turn, exact quadrant symmetry) at
+// offset 0 -- so the two ds_read2st64_b32 take the row offset b & 0xFFC as
+// is -- then 1025 {-2 ln c_j, 1/c_j} pairs (their base is the ds_read_b128's
+// immediate offset) and the exp2 table, 33 KB.  About 35 VALU per pair.  A 128-bit Philox block carries one pair and a 32-bit word
 // (the threshold lead of the one-lane and lane-group kernels); the lane-pair
 // kernel packs 5 pairs and two 16-bit leads into 4 blocks.  Accuracy:
 // tests/test_gpu_normals.py (libm form, NumPy).
 // ---------------------------------------------------------------------------
 constexpr int kBm64LogN = 1025, kBm64ScN = 1024, kExp2N = 64;
-constexpr int kBm64ExpOff = 2 * (kBm64LogN + kBm64ScN);   // 2^(i/64) table
+// layout in doubles: sin/cos words [0, 2048), log rows [2048, 4098), exp2
+constexpr int kBm64LogOff = 2 * kBm64ScN;                  // {-2 ln c, 1/c} rows
+constexpr int kBm64ExpOff = kBm64LogOff + 2 * kBm64LogN;   // 2^(i/64) table
 constexpr int kBm64Doubles = kBm64ExpOff + kExp2N;         // 4162 doubles
 
 __device__ __forceinline__ uint32_t hi32(double v) {
@@ -266,10 +303,25 @@ __device__ __forceinline__ double from_words(uint32_t hi, uint32_t lo) {
 
 // Copies the global table block (pbh_engine's bm64_tables) into LDS; every
 // thread of the workgroup takes part, then one barrier.
+// All of a thread's loads are issued before the first LDS write (one
+// global-memory round trip per launch instead of one per 4 KB slice: the
+// rolled loop waited for each load in turn, several microseconds of every
+// short launch).  Complete for blocks of >= 256 threads (all kernels here
+// run 256).
 __device__ __forceinline__ void bm64_load(double *lds, const double *g) {
+  constexpr int N2 = kBm64Doubles / 2, T = 256, R = N2 / T;   // 8 full rounds
+  static_assert(N2 - R * T <= T, "one partial round");
+  const int t = (int)(threadIdx.x & (T - 1));   // >= 256 threads: duplicates
   const double2 *src = reinterpret_cast<const double2 *>(g);
   double2 *dst = reinterpret_cast<double2 *>(lds);
-  for (int i = threadIdx.x; i < kBm64Doubles / 2; i += blockDim.x) dst[i] = src[i];
+  double2 v[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = src[t + k * T];
+  const bool tail = t < N2 - R * T;
+  double2 w = tail ? src[t + R * T] : double2{0., 0.};
+#pragma unroll
+  for (int k = 0; k < R; ++k) dst[t + k * T] = v[k];
+  if (tail) dst[t + R * T] = w;
   __syncthreads();
 }
 
@@ -278,13 +330,21 @@ __device__ __forceinline__ void bm64_load(double *lds, const double *g) {
 // row {-2 ln c, 1/c}; q4 is -2 log1p(r) / r to degree 4.
 struct LogTerm { double r, T; int e; };
 
+__device__ __forceinline__ uint32_t bfe_6_15(uint32_t v) {
+  // v_bfe_u32 v, 6, 15 as written (LLVM turns a bfe of a masked value into a
+  // shift and a second mask, one VALU more)
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, 6, 15" : "=v"(r) : "v"(v));
+  return r;
+}
+
 __device__ __forceinline__ LogTerm log_term(double x, const double *tab) {
   const double m = __builtin_amdgcn_frexp_mant(x);                 // [1/2, 1)
   const int e = __builtin_amdgcn_frexp_exp(x);
   const uint32_t ch = (hi32(m) + 0x200u) & 0xFFFFFC00u;            // c (hi word)
   // row j = (ch - 0x3FE00000) >> 10: byte offset 16 j = bits [20:6] of ch
   const double2 lt = *reinterpret_cast<const double2 *>(
-      reinterpret_cast<const char *>(tab) + __builtin_amdgcn_ubfe(ch, 6, 15));
+      reinterpret_cast<const char *>(tab + kBm64LogOff) + bfe_6_15(ch));
   return LogTerm{(m - from_words(ch, 0u)) * lt.y, lt.x, e};
 }
 
@@ -306,14 +366,15 @@ __device__ __forceinline__ void bm96_pair(uint32_t a, uint32_t b, uint32_t c,
   const double base = __builtin_fma(de, -2.0 * 6.93147180369123816490e-01,
                                     __builtin_fma(de, -2.0 * 1.90821492927058770002e-10, lt.T));
   const double E = __builtin_fma(lt.r, q4(lt.r), base);             // > 0
-  // ---- sqrt(E): v_rsq_f64 + two Newton steps ----
+  // ---- sqrt(E) = t (1 + e/2 + 3e^2/8 + ...), t = E y, e = 1 - E y^2, y =
+  // v_rsq_f64(E) (|e| < 2^-21): the truncation 5e^3/16 < 2^-64, the rounding
+  // of t enters e and cancels to first order: within an ulp, 5 VALU + rsq ----
   const double yr = __builtin_amdgcn_rsq(E);
-  const double hy = 0.5 * yr;
-  double rr = E * yr;
-  rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
-  rr = __builtin_fma(__builtin_fma(-rr, rr, E), hy, rr);
+  const double tt = E * yr;
+  const double ee = __builtin_fma(-tt, yr, 1.0);
+  const double rr = __builtin_fma(tt * ee, __builtin_fma(ee, 0.375, 0.5), tt);
   // ---- (sin, cos) of the full-turn angle ----
-  const char *sct = reinterpret_cast<const char *>(tab + 2 * kBm64LogN) + (b & 0xFFCu);
+  const char *sct = reinterpret_cast<const char *>(tab) + (b & 0xFFCu);
   const uint32_t *scw = reinterpret_cast<const uint32_t *>(sct);
   const double2 sc{from_words(scw[kBm64ScN], scw[0]),
                    from_words(scw[3 * kBm64ScN], scw[2 * kBm64ScN])};
@@ -371,6 +432,25 @@ __device__ __forceinline__ void st_buf(double *base, uint32_t voff,
       __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
                                         (int)voff, (int)soff, 2);
+}
+
+// The same through a resource of exactly nbytes: a lane whose voff is at or
+// past nbytes writes nothing (the raw buffer range check), so a loop-
+// invariant offset of kNoStore masks a lane's store without a branch.
+constexpr uint32_t kNoStore = 0x80000000u;
+__device__ __forceinline__ void st_buf_n(double *base, uint32_t nbytes,
+                                         uint32_t voff, double v) {
+  typedef unsigned int u32x2_t __attribute__((__vector_size__(8)));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
+                                        (int)voff, 0, 2);
+}
+__device__ __forceinline__ void st_buf32_n(uint32_t *base, uint32_t nbytes,
+                                           uint32_t voff, uint32_t v) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)voff, 0, 0);
 }
 
 // Lane selects in the VOP3 (e64) encoding.  On gfx950 the VOP2 form

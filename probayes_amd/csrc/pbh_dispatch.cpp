@@ -313,20 +313,21 @@ hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
   return hipGetLastError();
 }
 
-// The bm64 tables (pbh_device.h): {-2 ln c_j, 1 / c_j} for c_j = (1024 + j) /
-// 2048, j = 0..1024, then sin(J 2 pi / 1024) and cos(J 2 pi / 1024), J =
-// 0..1023 (the first quadrant evaluated, the others by exact symmetry) as
-// four arrays of 32-bit words (sin lo, sin hi, cos lo, cos hi), then
+// The bm64 tables (pbh_device.h): sin(J 2 pi / 1024) and cos(J 2 pi / 1024),
+// J = 0..1023 (the first quadrant evaluated, the others by exact symmetry)
+// as four arrays of 32-bit words (sin lo, sin hi, cos lo, cos hi); then
+// {-2 ln c_j, 1 / c_j} for c_j = (1024 + j) / 2048, j = 0..1024; then
 // 2^(i/64), i = 0..63.  Evaluated in long double (64-bit significand) and
 // rounded once to double.
 void bm64_tables(double *out) {
+  double *lg = out + kBm64LogOff;
   for (int j = 0; j < kBm64LogN; ++j) {
     const double c = (1024 + j) / 2048.0;   // exact
-    out[2 * j] = (double)(-2.0L * logl((long double)c));
-    out[2 * j + 1] = 1.0 / c;
+    lg[2 * j] = (double)(-2.0L * logl((long double)c));
+    lg[2 * j + 1] = 1.0 / c;
   }
   const long double pi = 3.141592653589793238462643383279502884L;
-  uint32_t *sc = reinterpret_cast<uint32_t *>(out + 2 * kBm64LogN);
+  uint32_t *sc = reinterpret_cast<uint32_t *>(out);
   constexpr int N = kBm64ScN, Q = kBm64ScN / 4;   // entries, per quadrant
   auto put = [&](int J, double s, double c) {
     uint64_t bs, bc;

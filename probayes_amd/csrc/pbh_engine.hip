@@ -75,6 +75,7 @@ struct pbh_engine {
   // (hipExtLaunchKernel: 2 us less GPU time, 3-4 us more host enqueue and
   // ~7 us more wall per short launch, measured: profiles/r02j_events.jsonl)
   bool gmm_full = true;      // PBH_GMM_FULL=0: no steady-state quad kernel
+  bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -202,11 +203,16 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
+  if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
+  // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
+  // A/B switch for the markers' fences; default 0 = hipEventDefault)
+  unsigned ev_flags = 0;
+  if (const char *ef = std::getenv("PBH_EVENT_FLAGS")) ev_flags = (unsigned)std::strtoul(ef, nullptr, 0);
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-  if (err == hipSuccess) err = hipEventCreate(&e->ev0);
-  if (err == hipSuccess) err = hipEventCreate(&e->ev1);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev0, ev_flags);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev1, ev_flags);
   if (err == hipSuccess) {
     std::vector<double> tab(pbh::kBm64Doubles);
     pbh::bm64_tables(tab.data());
@@ -909,6 +915,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gibbs_lanes = e->gibbs_lanes;
   k.gmm_lanes = e->gmm_lanes;
   k.gmm_full = e->gmm_full ? 1 : 0;
+  k.pair_full = e->pair_full ? 1 : 0;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;

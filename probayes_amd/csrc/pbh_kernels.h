@@ -103,6 +103,7 @@ struct KArgs {
   int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
   int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
   int32_t gmm_full;    // the quad kernel's steady-state form is allowed
+  int32_t pair_full;   // the lane-pair kernel's steady-state form is allowed
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;

@@ -924,9 +924,33 @@ struct PairDraw {
   }
 };
 
-template <int D, int RNG, bool MOM, bool LOC0 = false>
+// The steady-state pair kernel's rare undecided step (the lead could not
+// decide): t's remaining 53 - 16 bits from a block of this step alone and
+// the exact fp64 ratio form, out of line (the loop keeps neither its
+// registers nor its code).
+__device__ __attribute__((noinline)) bool pair_exact(uint32_t seed_lo, uint32_t seed_hi,
+                                                     double log_npi, int64_t g,
+                                                     int64_t chain, int h,
+                                                     uint32_t t0, double lpp,
+                                                     double lp) {
+  const u32x4 w = philox4x32_10(ctr(0x40u + 16u * h, g, chain), seed_lo, seed_hi);
+  const double t = u01((t0 << 16) | (w.x >> 16), w.y);
+  return ratio_accept(lpp, lp, t, false, log_npi);
+}
+
+// FULL (PHILOX only; pair_full_form): the steady-state launch -- thin 1,
+// every record inside the trace, past step 1, log pscale, N a multiple of 32
+// (no padding lanes).  Whole step pairs run branch-free apart from the rare
+// exact decision, and the NEXT pair's Philox blocks and Box-Muller pairs are
+// computed in the same basic blocks as the current pair's two dependent
+// steps (software pipelining: the scheduler interleaves the independent
+// integer/fp64 draw chains with each step's density -> decision -> select
+// chain).  The same words and arithmetic as the general form: identical
+// chains (tests/test_gpu_parity.py).
+template <int D, int RNG, bool MOM, bool LOC0 = false, bool FULL = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_pair_kernel(KArgs a) {
+  static_assert(!FULL || (RNG == PBH_RNG_PHILOX && !MOM), "FULL: production Philox");
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
   constexpr int H = D / 2;
   constexpr bool PHX = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_PHILOX_FP32;
@@ -935,7 +959,6 @@ void mh_pair_kernel(KArgs a) {
   constexpr bool TAB = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   using PD = PairDraw<H, RNG>;
   __shared__ double s_bmt[TAB ? kBm64Doubles : 2];
-  if constexpr (TAB) bm64_load(s_bmt, a.bm64);
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   constexpr bool mom = MOM;   // running moments compiled in or out
   const int lane = threadIdx.x & 63;
@@ -985,6 +1008,9 @@ void mh_pair_kernel(KArgs a) {
   const int64_t chain = a.off + cc;
   Xo xs{0u, 0u, 0u, 0u};
   if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, h, cc);
+
+  // the LDS tables after the state's loads: all of them in flight at once
+  if constexpr (TAB) bm64_load(s_bmt, a.bm64);
 
   // record phase / index of the trace, advanced per step (no 64-bit
   // division in the loop): step g records iff (g + 1) % thin == 0, at
@@ -1172,6 +1198,138 @@ void mh_pair_kernel(KArgs a) {
           PD::draw(a, s_bmt, h, (a.g0 + s) >> 1, chain, cA, cB, ctA, ctB);
       }
       if (s < a.n_steps) step(s, cA, ctA, t1);
+    } else if constexpr (FULL) {
+        // ---- steady state: whole pairs (see FULL above the kernel) ----
+        constexpr int NW = 3 * H + 1, NB = (NW + 3) / 4, QA = (H + 1) / 2;
+        constexpr uint64_t kHi = 0xFFFFFFFF00000000ull;
+        // the state's range bit (|lp| <= 700) as a lane mask, carried by the
+        // selects (one compare per step instead of two)
+        uint64_t inl = __ballot(__builtin_fabs(lp) <= 700.);
+        // lp rows: the lower half's lanes write nothing (range check)
+        const uint32_t lpoff = hi ? loff : kNoStore;
+        const uint32_t lpbytes = (uint32_t)(a.n * 8);
+        const uint32_t aoff = lane == 32 ? (uint32_t)((c >> 5) * 4) : kNoStore;
+        const uint32_t abytes = (uint32_t)(a.W * 8);
+        int64_t rec = a.g0 + s - a.rec_base;   // thin 1: record = step
+        const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);
+        auto philox = [&](int64_t P, uint32_t (&w)[4 * NB]) {
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            const u32x4 b = philox4x32_10_rk(ctr(q + 16 * h, P, chain), rk);
+            w[4 * q] = b.x;
+            w[4 * q + 1] = b.y;
+            w[4 * q + 2] = b.z;
+            w[4 * q + 3] = b.w;
+          }
+        };
+        // Box-Muller pairs q0 <= q < q1 of a pair's words into the two steps'
+        // normals (PairDraw's layout)
+        auto normals = [&](const uint32_t (&w)[4 * NB], auto Q0, auto Q1,
+                           double (&ra)[H], double (&rb)[H]) {
+          constexpr int q0 = decltype(Q0)::value, q1 = decltype(Q1)::value;
+#pragma unroll
+          for (int q = q0; q < q1; ++q) {
+            double z0, z1;
+            bm96_pair(w[3 * q], w[3 * q + 1], w[3 * q + 2], s_bmt, z0, z1);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int n = 2 * q + e;
+              const double z = e ? z1 : z0;
+              if (n < H) ra[n] = z;
+              else rb[n - H] = z;
+            }
+          }
+        };
+        auto step_full = [&](int si, const double (&r)[H], uint32_t t0) {
+          double xp[H];
+#pragma unroll
+          for (int i = 0; i < H; ++i)
+            xp[i] = LOC0 ? __builtin_fma(r[i], psc[i], x[i])
+                         : x[i] + __builtin_fma(r[i], psc[i], plc[i]);
+          double p0 = 0., p1 = 0.;
+#pragma unroll
+          for (int i = 0; i < H; ++i) {
+            const double u = __builtin_fma(xp[i], cb[i], -ca[i]);
+            if (i & 1) p1 = __builtin_fma(u, u, p1);
+            else p0 = __builtin_fma(u, u, p0);
+          }
+          double lo, up;
+          halves_f64(p0 + p1, lo, up);
+          const double lpp = (-(lo + up)) - a.ksum;
+          // accept_filter_lead_mask<16>, log pscale, the state's range bit
+          // carried in inl
+          const float eL = __builtin_amdgcn_exp2f(
+              (float)__builtin_fma(lpp - lp, 1.4426950408889634, 16.0));
+          const float fl = (float)t0;
+          const uint64_t inp = __ballot(__builtin_fabs(lpp) <= 700.);
+          const uint64_t inr = inp & inl;
+          const uint64_t af = __ballot(fl <= __builtin_fmaf(eL, 0.999996f, -1.0f));
+          const uint64_t rf = __ballot(fl > eL * 1.000004f);
+          uint64_t accm = inr & af;
+          const uint64_t needm = ~(inr & (af | rf)) & kHi;
+          if (needm) {   // wave-uniform, rare
+            bool ex = false;
+            if (__builtin_amdgcn_inverse_ballot_w64(needm))
+              ex = pair_exact(a.seed_lo, a.seed_hi, a.log_npi, a.g0 + si, chain, h,
+                              t0, lpp, lp);
+            accm = (accm & ~needm) | (__ballot(ex) & needm);
+          }
+          const uint64_t mhi = accm & kHi;
+          const uint64_t macc = mhi | (mhi >> 32);
+#pragma unroll
+          for (int i = 0; i < H; ++i) x[i] = sel_f64(macc, x[i], xp[i]);
+          lp = sel_f64(macc, lp, lpp);
+          inl = (inl & ~macc) | (inp & macc);
+          double *row = a.tx + rec * D * a.n;   // wave-uniform
+#pragma unroll
+          for (int i = 0; i < H; ++i) st_buf(row, boff, i * bstride, x[i]);
+          st_buf_n(a.tlp + rec * a.n, lpbytes, lpoff, lp);
+          st_buf32_n(reinterpret_cast<uint32_t *>(a.tacc + rec * a.W), abytes, aoff,
+                     (uint32_t)(mhi >> 32));
+          ++rec;
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using IA = std::integral_constant<int, QA>;
+        using IH = std::integral_constant<int, H>;
+        if (a.g0 & 1) {   // launch starts on a pair's 2nd step
+          uint32_t w[4 * NB];
+          philox(a.g0 >> 1, w);
+          normals(w, std::integral_constant<int, H / 2>{}, IH{}, cA, cB);
+          step_full(0, cB, w[3 * H] & 0xFFFFu);
+          s = 1;
+        }
+        if (s + 1 < a.n_steps) {
+          uint32_t w[4 * NB];
+          philox((a.g0 + s) >> 1, w);
+          normals(w, I0{}, IH{}, cA, cB);
+          ctA = w[3 * H] >> 16;
+          ctB = w[3 * H] & 0xFFFFu;
+          for (; s + 3 < a.n_steps; s += 2) {
+            uint32_t nw[4 * NB];
+            double nA[H], nB[H];
+            philox(((a.g0 + s) >> 1) + 1, nw);
+            step_full(s, cA, ctA);
+            normals(nw, I0{}, IA{}, nA, nB);
+            step_full(s + 1, cB, ctB);
+            normals(nw, IA{}, IH{}, nA, nB);
+#pragma unroll
+            for (int i = 0; i < H; ++i) {
+              cA[i] = nA[i];
+              cB[i] = nB[i];
+            }
+            ctA = nw[3 * H] >> 16;
+            ctB = nw[3 * H] & 0xFFFFu;
+          }
+          step_full(s, cA, ctA);
+          step_full(s + 1, cB, ctB);
+          s += 2;
+        }
+        if (s < a.n_steps) {   // launch ends on a pair's 1st step
+          uint32_t w[4 * NB];
+          philox((a.g0 + s) >> 1, w);
+          normals(w, I0{}, IA{}, cA, cB);
+          step_full(s, cA, w[3 * H] >> 16);
+        }
     } else {
       if (a.g0 & 1) {   // launch starts on a pair's 2nd step
         PD::draw(a, s_bmt, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
@@ -1565,15 +1723,18 @@ __device__ __forceinline__ float qperm_f32(float v) {
 // The rare undecided step of the quad kernel (accept_filter_ms32's need):
 // the exact ratio form of (lp', lp) on t's full 53 bits, out of line so that
 // the steady-state loop keeps neither its registers nor its code.
+// (Scalars, not the KArgs: a reference to the kernel arguments would make
+// the kernel copy all of them to its private stack at entry.)
 __device__ __attribute__((noinline)) bool gmm_quad_exact(
-    const KArgs &a, const double *tab, int64_t g, int64_t chain, uint32_t lead,
+    uint32_t seed_lo, uint32_t seed_hi, double acc_beta, double log_npi,
+    const double *tab, int64_t g, int64_t chain, uint32_t lead,
     double M, double S, double lm, double ls, double lp0) {
   constexpr int LB = kStepLead;
-  const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), a.seed_lo, a.seed_hi);
+  const u32x4 w = philox4x32_10(ctr(0x40u, g, chain), seed_lo, seed_hi);
   const double t = u01((lead << (32 - LB)) | (w.x >> LB), w.y);
   const double lpp = M + ln_tab(S, tab);
   const double lpc = lm == lp0 && ls == 1.0 ? lp0 : lm + ln_tab(ls, tab);
-  return ratio_accept(lpp * a.acc_beta, lpc * a.acc_beta, t, false, a.log_npi);
+  return ratio_accept(lpp * acc_beta, lpc * acc_beta, t, false, log_npi);
 }
 
 // FULL: the steady-state launch (gmm_quad_full): whole groups of 4 steps,
@@ -1588,7 +1749,6 @@ void mh_gmm_quad_kernel(KArgs a) {
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
   constexpr int LB = kStepLead;          // threshold lead bits (step_draws)
   __shared__ double s_bmt[kBm64Doubles];
-  bm64_load(s_bmt, a.bm64);
   const int lane = threadIdx.x & 63;
   const int p = lane & 3;
   const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1623,6 +1783,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   const uint32_t lpoff = (uint32_t)(((int64_t)p * a.n + cc) * 8);   // FULL
   double *txrow = a.tx + ri * D * a.n;   // record ri's rows (wave-uniform)
   const int64_t rstride = (int64_t)D * a.n;
+  bm64_load(s_bmt, a.bm64);        // after the state's loads: all in flight
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
 
   const int64_t gend = a.g0 + a.n_steps;
@@ -1687,7 +1848,8 @@ void mh_gmm_quad_kernel(KArgs a) {
         if (needm) {   // wave-uniform, rare
           bool ex = false;
           if (__builtin_amdgcn_inverse_ballot_w64(needm))
-            ex = gmm_quad_exact(a, s_bmt, g, chain, lead, M, S, lm, ls, lp0);
+            ex = gmm_quad_exact(a.seed_lo, a.seed_hi, a.acc_beta, a.log_npi, s_bmt,
+                                g, chain, lead, M, S, lm, ls, lp0);
           accm = (accm & ~needm) | (__ballot(ex) & needm);
         }
         acc = __builtin_amdgcn_inverse_ballot_w64(accm);
@@ -2402,8 +2564,27 @@ void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
                        block, lds, st, a);
 }
 
+// The lane-pair kernel's steady-state form applies (see mh_pair_kernel
+// FULL): production Philox, thin 1, every record of the launch inside the
+// trace, past step 1, log pscale, no padding lanes.  PBH_PAIR_FULL=0
+// (engine: pair_full) keeps the general form.
+inline bool pair_full_form(const KArgs &a) {
+  return a.pair_full && a.rng == PBH_RNG_PHILOX && a.has_pred && a.thin == 1 &&
+         a.pscale != PBH_PSCALE_LIN && a.tx != nullptr && a.n % 32 == 0 &&
+         a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
+}
+
 template <int D, bool MOM>
 void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
+  if constexpr (!MOM) {
+    if (pair_full_form(a)) {
+      if (a.ploc_zero)
+        pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX, false, true, true>), grid, block, 0, st, a);
+      else
+        pbh_launch((mh_pair_kernel<D, PBH_RNG_PHILOX, false, false, true>), grid, block, 0, st, a);
+      return;
+    }
+  }
   if (a.rng == PBH_RNG_REPLAY)
     pbh_launch((mh_pair_kernel<D, PBH_RNG_REPLAY, MOM>), grid, block, 0, st, a);
   else if (a.rng == PBH_RNG_PHILOX && a.ploc_zero)

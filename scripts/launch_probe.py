@@ -17,7 +17,7 @@ from probayes_amd import Engine  # noqa: E402
 
 
 def probe(rng, moments, steps, reps, sync_env, trace=True, chains=65536,
-          spl=250):
+          spl=250, tag=None):
   if sync_env:
     os.environ['PBH_SYNC'] = sync_env
   else:
@@ -42,7 +42,7 @@ def probe(rng, moments, steps, reps, sync_env, trace=True, chains=65536,
     kern.append(eng.last_run_ms()[0] / 1e3)
   eng.close()
   med = lambda v: float(np.median(v))
-  out = {'rng': rng, 'moments': moments, 'steps': steps, 'chains': chains,
+  out = {'tag': tag, 'rng': rng, 'moments': moments, 'steps': steps, 'chains': chains,
          'sync': sync_env or 'spin',
          'trace': trace, 'spl': spl, 'wall_us': med(walls) * 1e6,
          'enqueue_us': med(enq) * 1e6, 'kernel_us': med(kern) * 1e6,
@@ -54,6 +54,11 @@ def probe(rng, moments, steps, reps, sync_env, trace=True, chains=65536,
 
 
 if __name__ == '__main__':
+  if len(sys.argv) > 1:   # quick form: launch_probe.py TAG STEPS[,STEPS...]
+    tag = sys.argv[1]
+    for st in [int(v) for v in sys.argv[2].split(',')]:
+      out = probe('philox', False, st, 40, None, spl=250, tag=tag)
+    sys.exit(0)
   for rng in ('philox', 'philox_fp32'):
     for mom in (False, True):
       probe(rng, mom, 20, 30, None)

@@ -465,6 +465,43 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
       assert np.array_equal(ma[k], mb[k]), k
 
 
+@pytest.mark.parametrize('which', ['golden', 'bench'])
+def test_pair_steady_state_form_is_the_general_form(monkeypatch, which):
+  """The lane-pair kernel's steady-state launch (FULL: whole step pairs,
+  branch-free stores, the next pair's draws pipelined beside the current
+  pair's steps, the state's range bit carried as a mask) is bit-for-bit the
+  general form (PBH_PAIR_FULL=0): launches starting and ending on either step
+  of a pair, chains far in the tails (|lp| > 700: the exact decision), the
+  golden diag10 spec (nonzero proposal loc) and the bench's cfg2 spec."""
+  import bench
+  from probayes_amd import Engine
+  spec = oracle.golden_spec('diag10') if which == 'golden' else bench.cfg2_spec()
+  n, t = 4096, 61
+  init = np.zeros((n, 10)) if which == 'bench' else golden_init('diag10', n)
+  init[::97] += 40.   # log-density far below -700
+  outs = {}
+  for full in ('1', '0'):
+    monkeypatch.setenv('PBH_PAIR_FULL', full)
+    eng = Engine(spec)
+    eng.init_chains(init)
+    eng.set_rng('philox', seed=11)
+    eng.alloc_trace(t, 1)
+    eng.run(1)
+    eng.run(4, steps_per_launch=1)
+    eng.run(t - 5, steps_per_launch=13)
+    outs[full] = (eng.trace(), eng.state())
+    eng.close()
+  (ta, sa), (tb, sb) = outs['1'], outs['0']
+  for k in ('v_x', 'v_p', 'u'):
+    assert np.array_equal(ta[k], tb[k]), k
+  assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+  assert 0 < tb['u'].mean() < 1
+  # past step 1 the far chains never move: both densities underflow the
+  # ratio form's exp (rescale -> 0), so the exact decision rejects, as the
+  # reference's sp_utils.py ratio does
+  assert tb['u'][::97, 1:].max() == 0
+
+
 @pytest.mark.parametrize('name,thin,spl', [('diag10', 3, 0), ('diag10', 4, 7),
                                            ('gmm2', 4, 9), ('gibbs8', 5, 13),
                                            ('gibbs_sweep2', 3, 5)])
