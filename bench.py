@@ -159,6 +159,18 @@ def measured_traffic(chains, launch_steps, rng, trace):
   return None
 
 
+def kernel_label(args, n):
+  """The kernel the timed launches run (the engine's dispatch rules,
+  pbh_kernels_impl.h launch_mh_pair_m / pair_full_form)."""
+  if os.environ.get('PBH_NO_PAIR'):
+    return 'mh_kernel<10, {}, DIAG, GAUSS>'.format(args.rng.upper())
+  mom = int(args.moments or args.no_trace)
+  full = (args.rng == 'philox' and not mom and n % 32 == 0 and
+          os.environ.get('PBH_PAIR_FULL', '1') != '0')
+  return 'mh_pair_kernel<10, {}, MOM={}{}>'.format(args.rng.upper(), mom,
+                                                  ', FULL' if full else '')
+
+
 class EngineCollective:
   """The engine's own RCCL collectives (pbh_rccl_*): the production path."""
 
@@ -173,7 +185,7 @@ class EngineCollective:
 
 
 def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
-             trace=True, moments=False, seed=20261015):
+             trace=True, moments=False, seed=20261015, warmup_spl=None):
   """One rank of the bench (weak scaling: chains_per_gpu chains per rank):
   shard the global chain ids, warm up, time exactly `steps` steps between
   barriers, take the max over ranks, then collect the per-chain statistics
@@ -196,16 +208,17 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
   if warmup:
     # a short warm-up runs as one-step launches, so that the dispatch path
     # the timed launch takes has been exercised (same step count)
-    eng.run(warmup, steps_per_launch=1 if warmup <= 16 else spl)
+    eng.run(warmup, steps_per_launch=warmup_spl or (1 if warmup <= 16 else spl))
   barrier()
   t0 = time.perf_counter()
   eng.run(steps, steps_per_launch=spl, sync=False)
+  t1 = time.perf_counter()
   eng.sync()
   el = time.perf_counter() - t0
   kern_ms, launches = eng.last_run_ms()
   barrier()
   out = {'n': n, 'offset': offset, 'el': el, 'kern_ms': kern_ms,
-         'launches': launches}
+         'launches': launches, 'enqueue_s': t1 - t0}
   if col is not None:
     out['el'] = col.allreduce_max(el)
     t1 = time.perf_counter()
@@ -232,6 +245,9 @@ def main():
                   help='keep in-kernel running moments (off: the trace is '
                   'reduced on the device after the timed region)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--warmup-spl', type=int, default=None,
+                  help='steps per warm-up launch (default: 1 for a warm-up '
+                  'of <= 16 steps, else --steps-per-launch)')
   ap.add_argument('--traffic-bytes', type=float, default=None,
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
   args = ap.parse_args()
@@ -262,7 +278,8 @@ def main():
     col = EngineCollective(eng)
   spl = args.steps_per_launch
   res = run_rank(eng, col, rank, world, args.chains, args.steps, args.warmup,
-                 spl, args.rng, trace=not args.no_trace, moments=args.moments)
+                 spl, args.rng, trace=not args.no_trace, moments=args.moments,
+                 warmup_spl=args.warmup_spl)
   n, el, kern_ms, launches = res['n'], res['el'], res['kern_ms'], res['launches']
   collect_ms = res.get('collect_ms')
   if 'stats' in res:   # every chain of every rank, once
@@ -297,13 +314,14 @@ def main():
                                     n, min(spl, args.steps), args.rng,
                                     not args.no_trace),
                      'bytes_per_chain_step': bpcs,
-                     'kernel': ('mh_pair_kernel<10, {}, MOM={}>'.format(
-                         args.rng.upper(), int(args.moments or args.no_trace))
-                         if not os.environ.get('PBH_NO_PAIR') else
-                         'mh_kernel<10, {}, DIAG, GAUSS>'.format(args.rng.upper())),
+                     'kernel': kernel_label(args, n),
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),
+        # where the timed region's wall time went (rank 0): the host enqueue
+        # of the launches, the HIP-event time of the launches
+        'host_enqueue_us': res['enqueue_s'] * 1e6,
+        'events_us': kern_ms * 1e3,
     }
     if collect_ms is not None:
       line['rccl_allgather_ms'] = collect_ms

@@ -304,9 +304,234 @@ __global__ __launch_bounds__(256) void trace_ess_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same estimator through FFTs, the host's own method (ess_ips: rfft at
+// length 2T, |F|^2, irfft): one workgroup per PAIR of series (a, b) --
+// z_t = (a_t - mean a) + i (b_t - mean b) zero-padded to N = 4096 >= 2T, one
+// complex FFT, the two power spectra unpacked (X_k = (Z_k + conj Z_{N-k}) / 2,
+// Y_k = (Z_k - conj Z_{N-k}) / 2i) and packed again as P_k = |X_k|^2 + i
+// |Y_k|^2, one inverse FFT: Re / Im of the result are N x the two series'
+// autocovariance sums at every lag (no wrap: N >= 2T).  Then Geyer's pairs
+// (rho_{2j+1} + rho_{2j+2}, rho = ac / ac_0) summed up to the first non-
+// positive one, found by a block-wide min.  O(T log T) per series instead of
+// O(T x lags): the GMM chains of cfg5 need a few hundred lags.
+// FFT: Stockham autosort, radix 16 (4096 = 16^3, three passes, 256 threads
+// x 16 points in registers, the 16-point DFT as 4 x 4), in place in LDS
+// (rows padded by one entry per 16: fewer bank conflicts on the strided
+// writes).  Twiddles: one sincospi per pass and thread, powers by products.
+// Series s (= k n + c) and s + 1 are adjacent doubles of every record, so a
+// lane reads both with one 16-byte load; workgroups are mapped so that
+// consecutive pairs share an XCD (and its L2) -- the reads of one record row
+// by neighbouring pairs then hit the same L2 lines.
+// ---------------------------------------------------------------------------
+constexpr int kFftN = 4096, kFftT = 256;   // points, threads
+struct cdbl { double re, im; };
+__device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+__device__ __forceinline__ cdbl cadd(cdbl a, cdbl b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cdbl csub(cdbl a, cdbl b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cdbl cmul(cdbl a, cdbl b) {
+  return {__builtin_fma(a.re, b.re, -(a.im * b.im)), __builtin_fma(a.re, b.im, a.im * b.re)};
+}
+// times SIGN i
+template <int SIGN>
+__device__ __forceinline__ cdbl cmuli(cdbl a) {
+  return SIGN > 0 ? cdbl{-a.im, a.re} : cdbl{a.im, -a.re};
+}
+template <int SIGN>
+__device__ __forceinline__ void dft4(cdbl &a0, cdbl &a1, cdbl &a2, cdbl &a3) {
+  const cdbl t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3);
+  const cdbl t3 = cmuli<SIGN>(csub(a1, a3));
+  a0 = cadd(t0, t2);
+  a2 = csub(t0, t2);
+  a1 = cadd(t1, t3);
+  a3 = csub(t1, t3);
+}
+// 16-point DFT (exponent sign SIGN) of v; X[k1 + 4 k2] lands in v[4 k1 + k2]
+template <int SIGN>
+__device__ __forceinline__ void dft16(cdbl (&v)[16]) {
+  constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173;
+  constexpr double C2 = 0.70710678118654752440;
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) dft4<SIGN>(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+  // v[4 k1 + n2] *= W16^(SIGN n2 k1)
+  const cdbl w1{C1, SIGN * S1}, w2{C2, SIGN * C2}, w3{S1, SIGN * C1};
+  const cdbl w6{-C2, SIGN * C2}, w9{-C1, -SIGN * S1};
+  v[5] = cmul(v[5], w1);
+  v[6] = cmul(v[6], w2);
+  v[7] = cmul(v[7], w3);
+  v[9] = cmul(v[9], w2);
+  v[10] = cmuli<SIGN>(v[10]);
+  v[11] = cmul(v[11], w6);
+  v[13] = cmul(v[13], w3);
+  v[14] = cmul(v[14], w6);
+  v[15] = cmul(v[15], w9);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) dft4<SIGN>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+}
+// One Stockham pass (sub-transform size NS -> 16 NS), in place: all loads,
+// barrier, all stores, barrier.
+template <int SIGN, int NS>
+__device__ __forceinline__ void fft_pass(cdbl *buf) {
+  const int j = (int)threadIdx.x;
+  cdbl v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = buf[fpad(j + r * kFftT)];
+  if constexpr (NS > 1) {
+    const int m = j % NS;
+    double sn, cs;
+    sincospi((double)(SIGN * 2 * m) / (double)(16 * NS), &sn, &cs);
+    const cdbl w{cs, sn};
+    cdbl wr = w;
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      v[r] = cmul(v[r], wr);
+      if (r < 15) wr = cmul(wr, w);
+    }
+  }
+  dft16<SIGN>(v);
+  __syncthreads();
+  const int base = (j / NS) * NS * 16 + (j % NS);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) buf[fpad(base + (k1 + 4 * k2) * NS)] = v[4 * k1 + k2];
+  __syncthreads();
+}
+template <int SIGN>
+__device__ __forceinline__ void fft4096(cdbl *buf) {
+  fft_pass<SIGN, 1>(buf);
+  fft_pass<SIGN, 16>(buf);
+  fft_pass<SIGN, 256>(buf);
+}
+
+// block-wide sum / min over the 256 threads (red: 8 scratch entries)
+__device__ __forceinline__ double block_sum(double v, double *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__device__ __forceinline__ int block_min(int v, int *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return min(min(red[0], red[1]), min(red[2], red[3]));
+}
+
+__global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
+    const double *tx, int64_t n, int32_t d, int64_t first, int32_t T, double *ess) {
+  __shared__ cdbl buf[kFftN + kFftN / 16];
+  __shared__ double red[8];
+  __shared__ int ired[8];
+  // XCD-aware pair index: block b runs on XCD b % 8; give each XCD a
+  // contiguous range of pairs
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  const int64_t per = nb / 8, rem = nb % 8, xcd = b % 8, idx = b / 8;
+  const int64_t P = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+  const int64_t S = (int64_t)d * n;
+  const int64_t s0 = 2 * P;
+  const bool has_b = s0 + 1 < S;
+  const int j = (int)threadIdx.x;
+  const int64_t row = (int64_t)d * n;
+  const double *src = tx + first * row + s0;
+  // ---- load (t = j + 256 q, q < 8: T <= 2048) and centre ----
+  double xa[8], xb[8];
+  double sa = 0., sb = 0.;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int t = j + q * kFftT;
+    xa[q] = 0.;
+    xb[q] = 0.;
+    if (t < T) {
+      if (has_b) {
+        const double2 v = *reinterpret_cast<const double2 *>(src + (int64_t)t * row);
+        xa[q] = v.x;
+        xb[q] = v.y;
+      } else {
+        xa[q] = src[(int64_t)t * row];
+      }
+    }
+    sa += xa[q];
+    sb += xb[q];
+  }
+  const double ma = block_sum(sa, red) / (double)T;
+  const double mb = block_sum(sb, red + 4) / (double)T;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int t = j + q * kFftT;
+    cdbl z{0., 0.};
+    if (q < 8 && t < T) z = cdbl{xa[q] - ma, has_b ? xb[q] - mb : 0.};
+    buf[fpad(t)] = z;
+  }
+  __syncthreads();
+  fft4096<-1>(buf);
+  // ---- unpack the two spectra, pack |X|^2 + i |Y|^2 ----
+  cdbl pk[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = j + q * kFftT;
+    const cdbl zk = buf[fpad(k)], zm = buf[fpad((kFftN - k) & (kFftN - 1))];
+    const double xr = zk.re + zm.re, xi = zk.im - zm.im;   // 2 X_k
+    const double yr = zk.im + zm.im, yi = zm.re - zk.re;   // 2 Y_k
+    pk[q] = cdbl{__builtin_fma(xr, xr, xi * xi), __builtin_fma(yr, yr, yi * yi)};
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) buf[fpad(j + q * kFftT)] = pk[q];
+  __syncthreads();
+  fft4096<1>(buf);
+  // ---- Geyer's initial positive sequence on both series ----
+  const double a0 = buf[0].re, b0 = buf[0].im;
+  const double ia = 1.0 / (a0 > 1e-300 ? a0 : 1e-300);
+  const double ib = 1.0 / (b0 > 1e-300 ? b0 : 1e-300);
+  const int m = (T - 1) / 2;   // pairs (lags 2J + 1, 2J + 2), J < m
+  double pa[4], pb[4];
+  int fa = m, fb = m;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int J = j + q * kFftT;
+    pa[q] = pb[q] = 0.;
+    if (J < m) {
+      const cdbl u = buf[fpad(2 * J + 1)], v = buf[fpad(2 * J + 2)];
+      pa[q] = u.re * ia + v.re * ia;
+      pb[q] = u.im * ib + v.im * ib;
+      if (pa[q] <= 0. && J < fa) fa = J;
+      if (pb[q] <= 0. && J < fb) fb = J;
+    }
+  }
+  fa = block_min(fa, ired);
+  fb = block_min(fb, ired + 4);
+  double qa = 0., qb = 0.;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int J = j + q * kFftT;
+    if (J < fa) qa += pa[q];
+    if (J < fb) qb += pb[q];
+  }
+  qa = block_sum(qa, red);
+  qb = block_sum(qb, red + 4);
+  if (j == 0) {
+    const double da = 1.0 + 2.0 * qa, db = 1.0 + 2.0 * qb;
+    ess[s0] = (double)T / (da > 1e-12 ? da : 1e-12);
+    if (has_b) ess[s0 + 1] = (double)T / (db > 1e-12 ? db : 1e-12);
+  }
+}
+
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
-                            hipStream_t st) {
+                            hipStream_t st, bool fft) {
+  if (fft && count <= kFftN / 2) {
+    const int64_t pairs = ((int64_t)d * n + 1) / 2;
+    hipLaunchKernelGGL(trace_ess_fft_kernel, dim3((unsigned)pairs), dim3(kFftT), 0, st,
+                       tx, n, d, first, (int32_t)count, ess);
+    return hipGetLastError();
+  }
   const int64_t m = 4 * (int64_t)d * n;   // a quad of lanes per series
   hipLaunchKernelGGL(trace_ess_kernel, dim3((unsigned)((m + 255) / 256)),
                      dim3(256), 0, st, tx, n, d, first, count, ess);

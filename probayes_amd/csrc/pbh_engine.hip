@@ -76,6 +76,7 @@ struct pbh_engine {
   // ~7 us more wall per short launch, measured: profiles/r02j_events.jsonl)
   bool gmm_full = true;      // PBH_GMM_FULL=0: no steady-state quad kernel
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
+  bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -204,6 +205,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
+  if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
@@ -1249,7 +1251,8 @@ int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
     return fail(PBH_ERR_ARG, "ESS needs >= 2 records inside [0, %lld), got [%lld, %lld)",
                 (long long)rec, (long long)first, (long long)(first + count));
   HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(pbh::launch_trace_ess(e->tx, e->n, e->d, first, count, e->ess, e->stream));
+  HIP_TRY(pbh::launch_trace_ess(e->tx, e->n, e->d, first, count, e->ess, e->stream,
+                                e->ess_fft));
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (ess)
     HIP_TRY(hipMemcpy(ess, e->ess, (size_t)e->d * e->n * sizeof(double),

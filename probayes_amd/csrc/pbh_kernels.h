@@ -139,9 +139,10 @@ hipError_t launch_trace_expectation(const double *tx, const double *tlp,
                                     int64_t n, int32_t d, int64_t first,
                                     int64_t count, double exponent, int32_t lin,
                                     double log_npi, double *out, hipStream_t s);
+// fft: the FFT form for count <= 2048 records (else the direct-sum kernel)
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
-                            hipStream_t st);
+                            hipStream_t st, bool fft = true);
 // Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
 void bm64_tables(double *out);
 // Legacy (NumPy RandomState) stream generation (pbh_legacy.hip).

@@ -1,0 +1,21 @@
+# rocprofv3 evidence for the headline bench (run on the GPU box from the repo
+# root): for the driver's shape (--steps 20 --warmup 5: one 20-step timed
+# launch) and the default shape (1000 steps in 250-step launches), a kernel
+# trace + stats pass and separate FETCH_SIZE / WRITE_SIZE passes; the bench
+# JSON lines themselves.
+set -e
+export TMPDIR=/tmp
+R=$PWD
+OUT=$R/gpurun_out/prof3
+rm -rf $OUT && mkdir -p $OUT
+cd /tmp
+for S in s20 s1000; do
+  mkdir -p $OUT/$S
+  if [ $S = s20 ]; then ARGS="--steps 20 --warmup 5 --no-cpu-baseline"; else ARGS="--steps 1000 --warmup 250 --no-cpu-baseline"; fi
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$S/trace -o run -- python3 $R/bench.py $ARGS > $OUT/$S/bench_trace.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$S/fetch -o run -- python3 $R/bench.py $ARGS > $OUT/$S/bench_fetch.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$S/write -o run -- python3 $R/bench.py $ARGS > $OUT/$S/bench_write.log 2>&1
+  timeout -k 10 200 python3 $R/bench.py $ARGS > $OUT/$S/bench.log 2>&1
+done
+cd $R
+timeout -k 10 300 python3 bench.py > $OUT/bench_default.log 2>&1
