@@ -205,10 +205,16 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
     if col is not None:
       col.allreduce_max(0.0)
 
-  if warmup:
-    # a short warm-up runs as one-step launches, so that the dispatch path
-    # the timed launch takes has been exercised (same step count)
-    eng.run(warmup, steps_per_launch=warmup_spl or (1 if warmup <= 16 else spl))
+  if warmup and warmup_spl is None and warmup <= 16:
+    # a short warm-up runs as one-step runs, one pbh_run call each, so that
+    # the host path the timed launch takes (ctypes -> pbh_run -> event
+    # records -> launch) has run several times: the first timed enqueue is
+    # 10-12 us after a single warm-up call, 7-8 us after this
+    # (profiles/r03g_s20probe.jsonl)
+    for _ in range(warmup):
+      eng.run(1)
+  elif warmup:
+    eng.run(warmup, steps_per_launch=warmup_spl or spl)
   barrier()
   t0 = time.perf_counter()
   eng.run(steps, steps_per_launch=spl, sync=False)

@@ -70,6 +70,7 @@ struct pbh_engine {
   double *bm64 = nullptr;
   double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
   bool spin_sync = true;     // poll <= 2 ms, then block; PBH_SYNC=block: block
+  bool sync_event = false;   // PBH_SYNC=event: poll the last run's end event
   // timing events as marker packets around the launches (default), or
   // PBH_EVENT_MARKERS=0: on the first / last dispatch packet
   // (hipExtLaunchKernel: 2 us less GPU time, 3-4 us more host enqueue and
@@ -201,7 +202,10 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gf = std::getenv("PBH_GIBBS_FAST")) e->gibbs_fast = gf[0] != '0';
   if (const char *gl = std::getenv("PBH_GIBBS_LANES")) e->gibbs_lanes = std::atoi(gl);
   if (const char *ml = std::getenv("PBH_GMM_LANES")) e->gmm_lanes = std::atoi(ml);
-  if (const char *sy = std::getenv("PBH_SYNC")) e->spin_sync = std::strcmp(sy, "block") != 0;
+  if (const char *sy = std::getenv("PBH_SYNC")) {
+    e->spin_sync = std::strcmp(sy, "block") != 0;
+    e->sync_event = std::strcmp(sy, "event") == 0;
+  }
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
@@ -848,6 +852,19 @@ int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug
 
 int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  // PBH_TRACE_ENQUEUE=1: the host time of each enqueue phase to stderr
+  // (diagnostic of short-launch latency)
+  static const bool trace_enq = [] {
+    const char *t = std::getenv("PBH_TRACE_ENQUEUE");
+    return t && t[0] == '1';
+  }();
+  using clk = std::chrono::steady_clock;
+  const auto tq0 = clk::now();
+  auto tq = [&](const char *what) {
+    if (trace_enq)
+      std::fprintf(stderr, "pbh_run %s %.2f us\n", what,
+                   std::chrono::duration<double, std::micro>(clk::now() - tq0).count());
+  };
   if (!e->has_model || (!e->has_prop && !e->has_gibbs))
     return fail(PBH_ERR_STATE, "model and proposal/gibbs tables must be set");
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
@@ -929,8 +946,10 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   // the timed region: events on the first / last dispatch packet, or (with
   // PBH_EVENT_MARKERS=1) separate marker packets around the launches
   pbh::LaunchEvents &lev = pbh::launch_events();
+  tq("args");
   if (e->event_markers) {
     HIP_TRY(hipEventRecord(e->ev0, e->stream));
+    tq("event0");
     lev = {};
   } else {
     lev.start = e->ev0;
@@ -958,7 +977,9 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     ++launches;
   }
   lev = {};
+  tq("launches");
   if (e->event_markers) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  tq("event1");
   e->mom_steps += n_steps;
   e->timed = true;
   e->last_launches = launches;
@@ -975,6 +996,13 @@ int pbh_sync(pbh_engine *e) {
     // does not hold a host core at 100 %
     const auto t0 = std::chrono::steady_clock::now();
     hipError_t q;
+    // PBH_SYNC=event: the end event of the last run first (the stream's
+    // last packet when nothing was enqueued after it), then the stream
+    if (e->sync_event && e->timed) {
+      while ((q = hipEventQuery(e->ev1)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) break;
+      }
+    }
     while ((q = hipStreamQuery(e->stream)) == hipErrorNotReady) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) {
         q = hipStreamSynchronize(e->stream);

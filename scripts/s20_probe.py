@@ -18,7 +18,8 @@ from probayes_amd import Engine  # noqa: E402
 tag = sys.argv[1] if len(sys.argv) > 1 else ''
 # variants (environment): PROBE_PIN=1 pins the process to its first CPU,
 # PROBE_GC=0 disables the garbage collector, PROBE_WARM=k one-step warm-up
-# launches (default 5), PROBE_PRIME=1 reads the events once before timing
+# launches (default 5), PROBE_PRIME=1 reads the events once before timing,
+# PROBE_WARMLOOP=1 makes each warm-up step its own pbh_run call
 if os.environ.get('PROBE_PIN') == '1':
   os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
 if os.environ.get('PROBE_GC') == '0':
@@ -30,7 +31,11 @@ eng.init_chains(np.zeros((65536, bench.D)))
 eng.set_rng('philox', seed=7)
 eng.set_collect(moments=False)
 eng.alloc_trace(warm + 20 * 8, 1)
-eng.run(warm, steps_per_launch=1)
+if os.environ.get('PROBE_WARMLOOP') == '1':   # one pbh_run call per step
+  for _ in range(warm):
+    eng.run(1)
+else:
+  eng.run(warm, steps_per_launch=1)
 eng.sync()
 if os.environ.get('PROBE_PRIME') == '1':
   eng.last_run_ms()
