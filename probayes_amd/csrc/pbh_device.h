@@ -55,6 +55,11 @@ __device__ __forceinline__ uint32_t in_vgpr(uint32_t v) {
   asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(v));
   return r;
 }
+__device__ __forceinline__ double in_vgpr_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return __builtin_bit_cast(double, ((uint64_t)in_vgpr((uint32_t)(b >> 32)) << 32) |
+                                        in_vgpr((uint32_t)b));
+}
 __device__ __forceinline__ PhiloxKeys philox_keys_v(uint32_t k0, uint32_t k1) {
   PhiloxKeys k;
 #pragma unroll
@@ -419,6 +424,23 @@ __device__ __forceinline__ double exp_tab(double y, const double *tab) {
   const int ki = (int)k;
   const double t = tab[kBm64ExpOff + (ki & 63)];
   return __builtin_ldexp(t * p, ki >> 6);
+}
+
+// Production log / exp of a ufun dimension (x' = exp(log x + delta)) from the
+// same LDS tables: ln_tab's ~18 VALU against fast_log's ~35, exp_tab's ~16
+// against fast_exp's ~20.  Only the absolute accuracy of log x matters here
+// (it is exponentiated again): ~1e-16.  log: positive normal x through the
+// table, anything else through libm (a divergent branch no model value
+// takes); exp: any y, NaN propagated, +inf above 709.78, 0 below -746.
+__device__ __forceinline__ double ln_ufun(double x, const double *tab) {
+  const bool normal = x >= 2.2250738585072014e-308 && x <= 1.7976931348623157e308;
+  double r = ln_tab(normal ? x : 1.0, tab);
+  if (!normal) r = log(x);
+  return r;
+}
+__device__ __forceinline__ double exp_ufun(double y, const double *tab) {
+  const double e = exp_tab(__builtin_fmin(y, 710.0), tab);
+  return y != y ? y : (y > 709.782712893384 ? __builtin_inf() : e);
 }
 
 // Trace store through a buffer resource: base = a wave-uniform (SGPR)

@@ -78,6 +78,7 @@ struct pbh_engine {
   bool gmm_full = true;      // PBH_GMM_FULL=0: no steady-state quad kernel
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
+  bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -210,6 +211,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
+  if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
@@ -935,6 +937,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gmm_lanes = e->gmm_lanes;
   k.gmm_full = e->gmm_full ? 1 : 0;
   k.pair_full = e->pair_full ? 1 : 0;
+  k.iid_full = e->iid_full ? 1 : 0;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;

@@ -23,8 +23,11 @@ template <typename F, typename... Args>
 inline void pbh_launch(F kernel, const dim3 &grid, const dim3 &block,
                        size_t shm, hipStream_t st, Args... args) {
   LaunchEvents &ev = launch_events();
-  hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, st, ev.start,
-                        ev.stop, 0u, args...);
+  if (ev.start || ev.stop)   // events on the dispatch packet (PBH_EVENT_MARKERS=0)
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, st, ev.start,
+                          ev.stop, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, shm, st, args...);
   ev.start = nullptr;
 }
 
@@ -104,6 +107,7 @@ struct KArgs {
   int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
   int32_t gmm_full;    // the quad kernel's steady-state form is allowed
   int32_t pair_full;   // the lane-pair kernel's steady-state form is allowed
+  int32_t iid_full;    // cfg1's steady-state iid-Normal form is allowed
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;

@@ -440,8 +440,9 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   // FAST = production Philox path (fp32 normals, FMA-corrected divisions);
   // REPLAY and PHILOX_F64 keep the reference's arithmetic exactly.
   constexpr bool FAST = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
-  // production Gaussian deltas draw bm64 fp64 normals from LDS tables
-  constexpr bool TAB = FAST && (PROP == 0 || PROP == PBH_PROP_GAUSS);
+  // production Gaussian deltas draw bm64 fp64 normals from LDS tables; ufun
+  // dims take their log / exp from the same tables
+  constexpr bool TAB = FAST;
   const int prop = PROP ? PROP : a.prop;
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   const bool mom = a.moments != 0;
@@ -621,8 +622,10 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
         const double ss = np_sum_regs<D>(sq, D);
         if (FAST) {
           // production: the radius scale d0 / sqrt(ss) from one inverse
-          // square root (no IEEE sqrt and division on the step's chain)
-          const double sc = ss >= kNearlyPosZero ? d0 * rsq_nr(ss) : __builtin_inf();
+          // square root (no IEEE sqrt and division on the step's chain);
+          // rsq of max(ss, tiny) and a select, so that no branch is made
+          const double rq = rsq_nr(__builtin_fmax(ss, kNearlyPosZero));
+          const double sc = ss >= kNearlyPosZero ? d0 * rq : __builtin_inf();
 #pragma unroll
           for (int k = 0; k < D; ++k) dl[k] = (dl[k] * sc) * cld(a.plen, k);
         } else {
@@ -636,8 +639,8 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       for (int k = 0; k < D; ++k) {
         if ((a.ufun >> k) & 1u) {
           if (FAST) {
-            lxp[k] = fast_log(x[k]) + dl[k];
-            xp[k] = fast_exp(lxp[k]);
+            lxp[k] = ln_ufun(x[k], s_bmt) + dl[k];
+            xp[k] = exp_ufun(lxp[k], s_bmt);
           } else {
             xp[k] = exp(log(x[k]) + dl[k]);
           }
@@ -655,7 +658,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
                                 (a.bnd_xlo >> k) & 1u, (a.bnd_xhi >> k) & 1u);
           // a clamped / bounced ufun value: its log is taken afresh
           if (FAST && ((a.ufun >> k) & 1u) && !(xp[k] == v0))
-            lxp[k] = fast_log(xp[k]);
+            lxp[k] = ln_ufun(xp[k], s_bmt);
         }
       }
     }
@@ -744,6 +747,158 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       a.nacc[c] += nacc;
     }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cfg1's steady-state form (iid_full_form): the iid-Normal target (O(1)
+// sufficient statistics), the spherical tuple delta, production Philox, the
+// filtered ratio form, log pscale, thin 1, every record inside the trace,
+// past step 1, no tfun / int / bound dims; the ufun mask UFM compile-time.
+// mh_kernel's arithmetic and draws (the same joint_density, the same words),
+// without its per-step wave-uniform switches: the loop is one basic block
+// apart from the rare exact decision, the selects and stores take lane masks
+// (padding lanes write nothing: the buffer range check), and the kernel keeps
+// its uniform state in SGPRs without spilling them to VGPR lanes.  Identical
+// chains (test_iid_steady_state_form_is_the_general_form).
+// ---------------------------------------------------------------------------
+template <int D, int UFM>
+__global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
+  __shared__ double s_bmt[kBm64Doubles];
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t chain = a.off + cc;
+  double x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) x[k] = a.x[k * a.n + cc];
+  double lp = a.lp[cc];
+  double plen[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) plen[k] = cld(a.plen, k);
+  bm64_load(s_bmt, a.bm64);
+  __builtin_amdgcn_s_waitcnt(0);
+  const double d0 = a.sdelta;
+  const double beta = a.acc_beta;
+  // the density's constants (the prior bounds in VGPRs: SGPR pressure)
+  const int i0 = a.i0, i1 = a.i1;
+  const double tw0 = cld(a.tw, 0), tw1 = cld(a.tw, 1), nobs = (double)a.tn;
+  const double logC = a.norm_logC;
+  const bool has_prior = a.has_prior != 0;
+  const double prior_logp = a.prior_logp;
+  const uint32_t plo_incl = a.plo_incl, phi_incl = a.phi_incl;
+  double plo[D], phi[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    plo[k] = has_prior ? in_vgpr_f64(cld(a.plo, k)) : 0.;
+    phi[k] = has_prior ? in_vgpr_f64(cld(a.phi, k)) : 0.;
+  }
+  const uint32_t rowb = (uint32_t)(a.n * 8);
+  const uint32_t xoff = active ? (uint32_t)(c * 8) : kNoStore;
+  const uint32_t aoff = lane == 0 ? (uint32_t)((c >> 6) * 8) : kNoStore;
+  const uint32_t abytes = (uint32_t)(a.W * 8);
+  int64_t rec = a.g0 - a.rec_base;
+  const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);   // SGPRs stay free
+  for (int s = 0; s < a.n_steps; ++s, ++rec) {
+    const int64_t g = a.g0 + s;
+    // ---- draws: mh_kernel's production uniform draws ----
+    double r[D];
+    uint32_t lead = 0;
+#pragma unroll
+    for (int p = 0; p < (D + 1) / 2; ++p) {
+      const u32x4 w = philox4x32_10_rk(ctr(p, g, chain), rk);
+      r[2 * p] = u01(w.x, w.y);
+      if (2 * p + 1 < D) r[2 * p + 1] = u01(w.z, w.w);
+      if (p == 0)
+        lead = ((w.x & 31u) << 17) | ((w.y & 63u) << 11) |
+               (D >= 2 ? (((w.z & 31u) << 6) | (w.w & 63u)) : (w.z >> 21));
+    }
+    // ---- proposal: the spherical tuple delta, then the ufun ----
+    double dl[D], sq[D], xp[D], lxp[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      dl[k] = -d0 + (d0 - -d0) * r[k];
+      sq[k] = dl[k] * dl[k];
+    }
+    const double ss = np_sum_regs<D>(sq, D);
+    const double rq = rsq_nr(__builtin_fmax(ss, kNearlyPosZero));
+    const double sc = ss >= kNearlyPosZero ? d0 * rq : __builtin_inf();
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      dl[k] = (dl[k] * sc) * plen[k];
+      lxp[k] = 0.;
+      if (((UFM >> k) & 1) != 0) {   // folded per unrolled k
+        lxp[k] = ln_ufun(x[k], s_bmt) + dl[k];
+        xp[k] = exp_ufun(lxp[k], s_bmt);
+      } else {
+        xp[k] = x[k] + dl[k];
+      }
+    }
+    // joint_density<D, NORM_IID, FAST> restated on the preloaded constants
+    // (the same operations in the same order)
+    double lpp;
+    {
+      double mu = 0., sg = 1., l = 0.;
+      bool have = false;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        if (k == i0) mu = xp[k];
+        if (k == i1) sg = xp[k];
+        if (k == i1 && ((UFM >> k) & 1)) { l = lxp[k]; have = true; }
+      }
+      const double lsg = have ? l : fast_log(sg);
+      const double dm = tw0 - mu;
+      const double ssd = __builtin_fma(nobs * dm, dm, tw1);
+      const double s2 = sg * sg;
+      double ri = __builtin_amdgcn_rcp(s2);
+      ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+      ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+      double out = -0.5 * ssd * ri - nobs * (logC + lsg);
+      if (has_prior) {   // wave-uniform
+        // (x > lo) or (inclusive and x == lo): the reference's comparison
+        uint64_t in = ~0ull;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const uint64_t lo_ok = __ballot(xp[k] > plo[k]) |
+                                 (((plo_incl >> k) & 1u) ? __ballot(xp[k] == plo[k]) : 0ull);
+          const uint64_t hi_ok = __ballot(xp[k] < phi[k]) |
+                                 (((phi_incl >> k) & 1u) ? __ballot(xp[k] == phi[k]) : 0ull);
+          in &= lo_ok & hi_ok;
+        }
+        out = sel_f64(in, kNearlyNegInf, prior_logp) + out;
+      }
+      lpp = out;
+    }
+    // ---- the filtered ratio form of (beta lp', beta lp) ----
+    const double bA = lpp * beta, bB = lp * beta;
+    const DecisionMask dm = accept_filter_lead_mask<22>(bA, bB, lead, false);
+    uint64_t accm = dm.acc;
+    const uint64_t needm = dm.need & __ballot(true);
+    if (needm) {   // wave-uniform, rare
+      bool ex = false;
+      if (__builtin_amdgcn_inverse_ballot_w64(needm)) {
+        const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+        ex = ratio_accept(bA, bB, u01((lead << 10) | (w.x >> 22), w.y), false, a.log_npi);
+      }
+      accm = (accm & ~needm) | (__ballot(ex) & needm);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = sel_f64(accm, x[k], xp[k]);
+    lp = sel_f64(accm, lp, lpp);
+    // ---- trace: record rec = step - rec_base ----
+    double *row = a.tx + rec * D * a.n;   // wave-uniform
+#pragma unroll
+    for (int k = 0; k < D; ++k) st_buf_n(row + k * a.n, rowb, xoff, x[k]);
+    st_buf_n(a.tlp + rec * a.n, rowb, xoff, lp);
+    const uint64_t am = accm & __ballot(active);
+    st_buf_n(reinterpret_cast<double *>(a.tacc + rec * a.W), abytes, aoff,
+             __builtin_bit_cast(double, am));
+  }
+  if (active) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
+    a.lp[c] = lp;
   }
 }
 
@@ -1763,10 +1918,11 @@ void mh_gmm_quad_kernel(KArgs a) {
   const bool own = p < K;
   const double cw = own ? a.tw[p] : 0.;
   const double c0 = own ? a.tw[K + p] : -__builtin_inf();
-  double cmu[D], psc[D], plc[D];
+  // component term u = x w - mu w (mu w precomputed: one fma per dim)
+  double cmw[D], psc[D], plc[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) {
-    cmu[i] = own ? a.tb[p * D + i] : 0.;
+    cmw[i] = own ? a.tb[p * D + i] * cw : 0.;
     psc[i] = cld(a.pscl, i);
     plc[i] = cld(a.ploc, i);
   }
@@ -1787,10 +1943,21 @@ void mh_gmm_quad_kernel(KArgs a) {
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
 
   const int64_t gend = a.g0 + a.n_steps;
+  uint64_t inlm = __ballot(__builtin_fabs(lm) <= 698.);   // FULL: |lm| <= 698
+  // FULL: lane p < D writes dim p's record row, the others nothing (the
+  // buffer range check: no select of the dim, no branch)
+  uint32_t xoffm[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) xoffm[i] = p == i ? (uint32_t)(((int64_t)i * a.n + cc) * 8) : kNoStore;
+  const uint32_t rbytes = (uint32_t)(rstride * 8);
   for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
     // ---- lane p draws step 4 G + p; the quad shares the group's draws
     double rown[D];
     const uint32_t lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
+    // FULL: the threshold lead as the float the filter compares (the same
+    // value accept_filter_rel32 forms), converted once per group and lane
+    constexpr float kLw = 1.0f / (float)(1u << LB);
+    const float tlown = FULL ? (float)lown * kLw : 0.f;
     double gm[4], gs[4];     // the group's states (M, S), for the records
     int64_t grec[4];
     // FULL: the group's record rows as scalar buffer bases, one pair of
@@ -1804,7 +1971,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       double r[D];
 #pragma unroll
       for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
-      const uint32_t lead = qperm_u32<j * 85>(lown);
+      const uint32_t lead = FULL ? 0u : qperm_u32<j * 85>(lown);
       const int64_t g = 4 * G + j;
       grec[j] = -1;
       gm[j] = lm;
@@ -1817,7 +1984,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       double v = c0;
 #pragma unroll
       for (int i = 0; i < D; ++i) {
-        const double u = (xp[i] - cmu[i]) * cw;
+        const double u = __builtin_fma(xp[i], cw, -cmw[i]);
         v = __builtin_fma(-u, u, v);
       }
       // decision path: the terms relative to the state's max lm
@@ -1840,18 +2007,25 @@ void mh_gmm_quad_kernel(KArgs a) {
       bool acc;
       uint64_t accm = 0;   // FULL: the decisions as a lane mask
       if constexpr (FULL) {
-        const uint64_t inrm = __ballot(__builtin_fabs(M) <= 698.) &
-                              __ballot(__builtin_fabs(lm) <= 698.);
-        const DecisionMask dm = accept_filter_rel32_mask<LB>(E32, ls32, inrm, lead);
-        accm = dm.acc;
-        const uint64_t needm = dm.need & __ballot(true);
+        // the state's range bit is carried as a mask (inlm) through the
+        // selects; accept_filter_rel32_mask on the broadcast float lead
+        const uint64_t inMm = __ballot(__builtin_fabs(M) <= 698.);
+        const uint64_t inrm = inMm & inlm;
+        const float tlo = qperm_f32<j * 85>(tlown);
+        const float thi = tlo + kLw;
+        const uint64_t af = __ballot(thi * ls32 <= E32 * 0.999996f);
+        const uint64_t rf = __ballot(tlo * ls32 > E32 * 1.000004f);
+        accm = inrm & af;
+        const uint64_t needm = ~(inrm & (af | rf)) & __ballot(true);
         if (needm) {   // wave-uniform, rare
+          const uint32_t ld = qperm_u32<j * 85>(lown);
           bool ex = false;
           if (__builtin_amdgcn_inverse_ballot_w64(needm))
             ex = gmm_quad_exact(a.seed_lo, a.seed_hi, a.acc_beta, a.log_npi, s_bmt,
-                                g, chain, lead, M, S, lm, ls, lp0);
+                                g, chain, ld, M, S, lm, ls, lp0);
           accm = (accm & ~needm) | (__ballot(ex) & needm);
         }
+        inlm = (inlm & ~accm) | (inMm & accm);
         acc = __builtin_amdgcn_inverse_ballot_w64(accm);
       } else if (!a.has_pred && s == 0) {
         acc = true;                                  // s = None on step 1
@@ -1896,12 +2070,10 @@ void mh_gmm_quad_kernel(KArgs a) {
         mq = __builtin_fma(xo, xo, mq);
       }
       if constexpr (FULL) {
-        double xo = x[0];
-#pragma unroll
-        for (int i = 1; i < D; ++i) xo = p % D == i ? x[i] : xo;
         // the record row is wave-uniform: a scalar buffer resource (without
         // readfirstlane the compiler wraps the store in a waterfall loop)
-        st_buf(gtx, xoff, (uint32_t)(j * rstride * 8), xo);
+#pragma unroll
+        for (int i = 0; i < D; ++i) st_buf_n(gtx + j * rstride, rbytes, xoffm[i], x[i]);
         grec[j] = ri;
         uint64_t m = accm & 0x1111111111111111ull & act_bits;
         m = (m | (m >> 3)) & 0x0303030303030303ull;
@@ -2574,6 +2746,19 @@ inline bool pair_full_form(const KArgs &a) {
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }
 
+// cfg1's steady-state form applies (see mh_iid_full_kernel): production
+// Philox, the filtered ratio form, log pscale, thin 1, every record of the
+// launch inside the trace, past step 1, no tfun / int / bound dims, no
+// moments, a ufun mask of the kernel's d.  PBH_IID_FULL=0 (engine:
+// iid_full) keeps the general form.
+inline bool iid_full_form(const KArgs &a) {
+  return a.iid_full && a.rng == PBH_RNG_PHILOX && a.simple_acc && !a.debug &&
+         a.has_pred && a.thin == 1 && a.pscale != PBH_PSCALE_LIN && a.tx != nullptr &&
+         !a.has_tfun && a.vint == 0 && a.bnd_on == 0 && !a.moments &&
+         a.ufun < (1u << a.d) && a.n * 8 < (int64_t(1) << 31) &&
+         a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
+}
+
 template <int D, bool MOM>
 void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
   if constexpr (!MOM) {
@@ -2694,6 +2879,18 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
       return hipGetLastError();
     }
     if (a.target == PBH_TARGET_NORM_IID && a.prop == PBH_PROP_SPHERE) {
+      if constexpr (D <= 2) {
+        if (iid_full_form(a)) {
+          const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
+          switch (a.ufun) {
+            case 0: pbh_launch((mh_iid_full_kernel<D, 0>), grid, block, 0, st, a); break;
+            case 1: pbh_launch((mh_iid_full_kernel<D, 1>), grid, block, 0, st, a); break;
+            case 2: pbh_launch((mh_iid_full_kernel<D, 2>), grid, block, 0, st, a); break;
+            default: pbh_launch((mh_iid_full_kernel<D, 3>), grid, block, 0, st, a); break;
+          }
+          return hipGetLastError();
+        }
+      }
       launch_mh_spec<D, PBH_TARGET_NORM_IID, PBH_PROP_SPHERE>(a, st, lds);
       return hipGetLastError();
     }

@@ -465,6 +465,36 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
       assert np.array_equal(ma[k], mb[k]), k
 
 
+def test_iid_steady_state_form_is_the_general_form(monkeypatch):
+  """cfg1's steady-state launch (mh_iid_full_kernel: iid-Normal target,
+  spherical delta, ufun on sigma, uniform prior, e-tempered ratio form) is
+  bit-for-bit mh_kernel's general form (PBH_IID_FULL=0): a ragged chain
+  count (padding lanes write nothing), launches of 1 and 13 steps, chains
+  started outside the prior box (density -inf until they enter it)."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec('metrohast_norm1d')
+  n, t = 4096 + 5, 61
+  init = golden_init('metrohast_norm1d', n)
+  init[::89, 1] = 30.   # sigma outside (5, 20)
+  outs = {}
+  for full in ('1', '0'):
+    monkeypatch.setenv('PBH_IID_FULL', full)
+    eng = Engine(spec)
+    eng.init_chains(init)
+    eng.set_rng('philox', seed=13)
+    eng.alloc_trace(t, 1)
+    eng.run(1)
+    eng.run(4, steps_per_launch=1)
+    eng.run(t - 5, steps_per_launch=13)
+    outs[full] = (eng.trace(), eng.state())
+    eng.close()
+  (ta, sa), (tb, sb) = outs['1'], outs['0']
+  for k in ('v_x', 'v_p', 'u'):
+    assert np.array_equal(ta[k], tb[k]), k
+  assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+  assert 0 < tb['u'].mean() < 1
+
+
 @pytest.mark.parametrize('which', ['golden', 'bench'])
 def test_pair_steady_state_form_is_the_general_form(monkeypatch, which):
   """The lane-pair kernel's steady-state launch (FULL: whole step pairs,
