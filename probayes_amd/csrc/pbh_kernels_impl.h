@@ -1898,7 +1898,9 @@ __device__ __attribute__((noinline)) bool gmm_quad_exact(
 // first-step tests, and branch-free stores: a lane with nothing of its own
 // to write (a part p >= D, or a padding chain, which runs chain 0's exact
 // trajectory) rewrites the identical value of a lane that has.
-template <int D, int K, bool MOM, bool FULL>
+// LOC0: every proposal loc is 0 (the examples' norm.rvs(scale=...)): x' =
+// fma(r, scale, x), one rounding, instead of x + fma(r, scale, loc).
+template <int D, int K, bool MOM, bool FULL, bool LOC0 = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_gmm_quad_kernel(KArgs a) {
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
@@ -1950,10 +1952,45 @@ void mh_gmm_quad_kernel(KArgs a) {
 #pragma unroll
   for (int i = 0; i < D; ++i) xoffm[i] = p == i ? (uint32_t)(((int64_t)i * a.n + cc) * 8) : kNoStore;
   const uint32_t rbytes = (uint32_t)(rstride * 8);
+  // FULL: the draws are software-pipelined by group -- group G + 1's Philox
+  // block(s) are computed beside group G's first step and its Box-Muller
+  // pair(s) beside the second (step_draws' words and arithmetic, split)
+  constexpr int NP = (D + 1) / 2, NW = 3 * NP + 1, NB = (NW + 3) / 4;
+  double rnext[D];
+  uint32_t lnext = 0;
+  if constexpr (FULL) lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
   for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
     // ---- lane p draws step 4 G + p; the quad shares the group's draws
     double rown[D];
-    const uint32_t lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
+    uint32_t lown;
+    if constexpr (FULL) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) rown[i] = rnext[i];
+      lown = lnext;
+    } else {
+      lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
+    }
+    uint32_t wn[4 * NB];   // FULL: group G + 1's words
+    auto next_blocks = [&]() {
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const u32x4 b = philox4x32_10(ctr(q, 4 * (G + 1) + p, chain), a.seed_lo, a.seed_hi);
+        wn[4 * q] = b.x;
+        wn[4 * q + 1] = b.y;
+        wn[4 * q + 2] = b.z;
+        wn[4 * q + 3] = b.w;
+      }
+    };
+    auto next_normals = [&]() {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        double z0, z1;
+        bm96_pair(wn[3 * q], wn[3 * q + 1], wn[3 * q + 2], s_bmt, z0, z1);
+        rnext[2 * q] = z0;
+        if (2 * q + 1 < D) rnext[2 * q + 1] = z1;
+      }
+      lnext = wn[3 * NP] >> (32 - kStepLead);
+    };
     // FULL: the threshold lead as the float the filter compares (the same
     // value accept_filter_rel32 forms), converted once per group and lane
     constexpr float kLw = 1.0f / (float)(1u << LB);
@@ -1980,7 +2017,8 @@ void mh_gmm_quad_kernel(KArgs a) {
       const int s = (int)(g - a.g0);
       double xp[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) xp[i] = x[i] + __builtin_fma(r[i], psc[i], plc[i]);
+      for (int i = 0; i < D; ++i)
+        xp[i] = LOC0 ? __builtin_fma(r[i], psc[i], x[i]) : x[i] + __builtin_fma(r[i], psc[i], plc[i]);
       double v = c0;
 #pragma unroll
       for (int i = 0; i < D; ++i) {
@@ -2113,7 +2151,9 @@ void mh_gmm_quad_kernel(KArgs a) {
           reinterpret_cast<uint16_t *>(a.tacc)[rec * 4 * a.W + wave] = (uint16_t)m;
       }
     };
+    if constexpr (FULL) next_blocks();
     step(std::integral_constant<int, 0>{});
+    if constexpr (FULL) next_normals();
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
@@ -2825,6 +2865,17 @@ inline bool gmm_quad_full(const KArgs &a) {
 template <int D, bool MOM, bool FULL>
 void launch_gmm_quad(const KArgs &a, const dim3 &grid, const dim3 &block,
                      hipStream_t st) {
+  if constexpr (D == 2) {   // cfg5's d: the zero-loc form
+    if (a.ploc_zero) {
+      if (a.tn == 2)
+        pbh_launch((mh_gmm_quad_kernel<D, 2, MOM, FULL, true>), grid, block, 0, st, a);
+      else if (a.tn == 3)
+        pbh_launch((mh_gmm_quad_kernel<D, 3, MOM, FULL, true>), grid, block, 0, st, a);
+      else
+        pbh_launch((mh_gmm_quad_kernel<D, 4, MOM, FULL, true>), grid, block, 0, st, a);
+      return;
+    }
+  }
   if (a.tn == 2)
     pbh_launch((mh_gmm_quad_kernel<D, 2, MOM, FULL>), grid, block, 0, st, a);
   else if (a.tn == 3)
