@@ -2089,13 +2089,13 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int i = 0; i < D; ++i) x[i] = sel_f64(accm, x[i], xp[i]);
         lm = sel_f64(accm, lm, M);
         ls = sel_f64(accm, ls, S);
-        ls32 = sel_f32(accm, ls32, (float)S);
+        ls32 = (float)ls;   // fp32 of the selected S (no select of its own)
       } else {
 #pragma unroll
         for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
         lm = acc ? M : lm;
         ls = acc ? S : ls;
-        ls32 = acc ? (float)S : ls32;
+        ls32 = (float)ls;
       }
       gm[j] = lm;
       gs[j] = ls;
