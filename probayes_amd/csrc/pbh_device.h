@@ -459,6 +459,7 @@ __device__ __forceinline__ void st_buf(double *base, uint32_t voff,
 // The same through a resource of exactly nbytes: a lane whose voff is at or
 // past nbytes writes nothing (the raw buffer range check), so a loop-
 // invariant offset of kNoStore masks a lane's store without a branch.
+// Callers keep nbytes <= kNoStore (the launch conditions check it).
 constexpr uint32_t kNoStore = 0x80000000u;
 __device__ __forceinline__ void st_buf_n(double *base, uint32_t nbytes,
                                          uint32_t voff, double v) {

@@ -2783,6 +2783,7 @@ void launch_mh_spec(const KArgs &a, hipStream_t st, size_t lds) {
 inline bool pair_full_form(const KArgs &a) {
   return a.pair_full && a.rng == PBH_RNG_PHILOX && a.has_pred && a.thin == 1 &&
          a.pscale != PBH_PSCALE_LIN && a.tx != nullptr && a.n % 32 == 0 &&
+         a.n * 8 <= (int64_t)kNoStore &&   // masked stores: kNoStore out of range
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }
 
@@ -2795,7 +2796,7 @@ inline bool iid_full_form(const KArgs &a) {
   return a.iid_full && a.rng == PBH_RNG_PHILOX && a.simple_acc && !a.debug &&
          a.has_pred && a.thin == 1 && a.pscale != PBH_PSCALE_LIN && a.tx != nullptr &&
          !a.has_tfun && a.vint == 0 && a.bnd_on == 0 && !a.moments &&
-         a.ufun < (1u << a.d) && a.n * 8 < (int64_t(1) << 31) &&
+         a.ufun < (1u << a.d) && a.n * 8 <= (int64_t)kNoStore &&   // masked stores
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }
 
@@ -2858,6 +2859,7 @@ inline bool gmm_pair_form(const KArgs &a) {
 inline bool gmm_quad_full(const KArgs &a) {
   return a.gmm_full && a.has_pred && a.acc_beta == 1.0 && a.thin == 1 &&
          (int64_t)4 * a.d * a.n * 8 < (int64_t(1) << 32) &&   // group row offsets
+         (int64_t)a.d * a.n * 8 <= (int64_t)kNoStore &&      // masked stores
          a.tx != nullptr && a.g0 % 4 == 0 && a.n_steps % 4 == 0 &&
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }

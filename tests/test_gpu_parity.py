@@ -256,14 +256,18 @@ def _ess_ips(x):
   return t / np.maximum(1.0 + 2.0 * s, 1e-12), pairs, first
 
 
+@pytest.mark.parametrize('fft', ['1', '0'])
 @pytest.mark.parametrize('name,n,t,burn', [('gmm2', 2000, 600, 100),
-                                           ('diag10', 300, 257, 7)])
-def test_device_ess_and_trace_stats_match_host(name, n, t, burn):
-  """pbh_trace_ess (on-device initial positive sequence) equals the host FFT
-  estimator on the same trace within 1e-9 wherever the sequence's stopping
-  pair is not within rounding of zero; pbh_trace_stats equals the host sums
-  of the trace."""
+                                           ('diag10', 300, 257, 7),
+                                           ('gmm2', 33, 2100, 40)])
+def test_device_ess_and_trace_stats_match_host(monkeypatch, name, n, t, burn, fft):
+  """pbh_trace_ess (on-device initial positive sequence: the FFT kernel,
+  or with PBH_ESS_FFT=0 the direct-sum kernel; more than 2 048 records
+  always take the direct sums) equals the host FFT estimator on the same
+  trace within 1e-9 wherever the sequence's stopping pair is not within
+  rounding of zero; pbh_trace_stats equals the host sums of the trace."""
   from probayes_amd import Engine
+  monkeypatch.setenv('PBH_ESS_FFT', fft)
   spec = oracle.golden_spec(name)
   eng = Engine(spec)
   eng.init_chains(golden_init(name, n))
@@ -286,7 +290,7 @@ def test_device_ess_and_trace_stats_match_host(name, n, t, burn):
     m = pairs.shape[1]
     dec = np.abs(pairs[np.arange(len(first)), np.minimum(first, m - 1)])
     clear = dec > 1e-9
-    assert clear.mean() > 0.99
+    assert (~clear).sum() <= max(1, 0.01 * clear.size)
     rel = np.abs(dev[clear, k] / host[clear] - 1)
     assert rel.max() < 1e-9, rel.max()
 
