@@ -3,6 +3,8 @@
 // gfx950 code objects compile in parallel.
 #include <cstring>
 #include <cmath>
+#include <cstdlib>
+#include <unordered_map>
 
 #include "pbh_kernels.h"
 #include "pbh_device.h"
@@ -13,6 +15,24 @@ namespace pbh {
 LaunchEvents &launch_events() {
   static thread_local LaunchEvents ev;
   return ev;
+}
+
+bool module_launch() {
+  static const bool on = [] {
+    const char *m = std::getenv("PBH_MODULE_LAUNCH");
+    return !(m && m[0] == '0');
+  }();
+  return on;
+}
+
+hipFunction_t kernel_function(const void *kernel) {
+  static thread_local std::unordered_map<const void *, hipFunction_t> cache;
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  hipFunction_t fn = nullptr;
+  (void)hipGetFuncBySymbol(&fn, kernel);
+  cache.emplace(kernel, fn);
+  return fn;
 }
 
 

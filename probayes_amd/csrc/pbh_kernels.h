@@ -18,16 +18,28 @@ struct LaunchEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 LaunchEvents &launch_events();   // thread-local (pbh_dispatch.cpp)
+bool module_launch();            // not PBH_MODULE_LAUNCH=0 (pbh_dispatch.cpp)
+hipFunction_t kernel_function(const void *kernel);   // cached hipGetFuncBySymbol
 
 template <typename F, typename... Args>
 inline void pbh_launch(F kernel, const dim3 &grid, const dim3 &block,
                        size_t shm, hipStream_t st, Args... args) {
   LaunchEvents &ev = launch_events();
-  if (ev.start || ev.stop)   // events on the dispatch packet (PBH_EVENT_MARKERS=0)
-    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, st, ev.start,
-                          ev.stop, 0u, args...);
-  else
+  if (ev.start || ev.stop) {   // events on the dispatch packet (PBH_EVENT_MARKERS=0)
+    (void)hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, st, ev.start,
+                                ev.stop, 0u, args...);
+  } else if (const hipFunction_t fn = module_launch()
+                 ? kernel_function(reinterpret_cast<const void *>(kernel)) : nullptr) {
+    // hipModuleLaunchKernel on the kernel's hipFunction_t, cached per kernel:
+    // no per-launch symbol lookup (≈ 0.5 us less host enqueue per launch,
+    // profiles/r03o_s20probe.jsonl); PBH_MODULE_LAUNCH=0 keeps
+    // hipLaunchKernelGGL
+    void *params[] = {reinterpret_cast<void *>(&args)...};
+    (void)hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z,
+                                (unsigned)shm, st, params, nullptr);
+  } else {
     hipLaunchKernelGGL(kernel, grid, block, shm, st, args...);
+  }
   ev.start = nullptr;
 }
 
