@@ -25,13 +25,30 @@ bool module_launch() {
   return on;
 }
 
+// Keyed by (kernel, current device): a handle is resolved for the device
+// that is current when it is looked up (engines on several devices in one
+// process each get their own).  Null (the caller then takes
+// hipLaunchKernelGGL) when the lookup fails.
 hipFunction_t kernel_function(const void *kernel) {
-  static thread_local std::unordered_map<const void *, hipFunction_t> cache;
-  auto it = cache.find(kernel);
+  struct Key {
+    const void *k;
+    int dev;
+    bool operator==(const Key &o) const { return k == o.k && dev == o.dev; }
+  };
+  struct Hash {
+    size_t operator()(const Key &x) const {
+      return std::hash<const void *>()(x.k) ^ ((size_t)x.dev * 0x9E3779B97F4A7C15ull);
+    }
+  };
+  static thread_local std::unordered_map<Key, hipFunction_t, Hash> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const Key key{kernel, dev};
+  auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   hipFunction_t fn = nullptr;
-  (void)hipGetFuncBySymbol(&fn, kernel);
-  cache.emplace(kernel, fn);
+  if (hipGetFuncBySymbol(&fn, kernel) != hipSuccess) fn = nullptr;
+  cache.emplace(key, fn);
   return fn;
 }
 
