@@ -284,8 +284,10 @@ int pbh_reset_moments(pbh_engine *eng);
 /* Per-(chain, dim) effective sample size of trace records [first, first +
  * count) on the device: Geyer's initial positive sequence over the
  * autocorrelations of each centred series (the estimator behind cfg5's
- * ESS/s); ess [d][N] on the host (may be NULL).  The result
- * also stays in the engine for pbh_rccl_allgather_stats.                    */
+ * ESS/s); the autocorrelations by FFT (two series per
+ * 4 096-point transform, count <= 2 048; direct sums above that or with
+ * PBH_ESS_FFT=0); ess [d][N] on the host (may be NULL).  The result also
+ * stays in the engine for pbh_rccl_allgather_stats.                         */
 int pbh_trace_ess(pbh_engine *eng, int64_t first, int64_t count, double *ess);
 /* The same per-chain statistics reduced on the device from trace records
  * [first, first + count) (PD summate + expectation over a recorded trace,
