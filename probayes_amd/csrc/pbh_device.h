@@ -290,6 +290,51 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 // kernel packs 5 pairs and two 16-bit leads into 4 blocks.  Accuracy:
 // tests/test_gpu_normals.py (libm form, NumPy).
 // ---------------------------------------------------------------------------
+// Two waves share each SIMD in the steady-state kernels, and the SIMD's
+// arbiter issues the OLDER wave first among equal priorities: left alone, the
+// first workgroup generation finishes a 250-step cfg2 launch at 175 us and the
+// second runs on by itself, at one wave per SIMD, until 264 us
+// (profiles/r03_phase_*, scripts/phase_probe.py).  Alternating the priority
+// between the SIMD's two wave slots on a shared clock (the 100 MHz real-time
+// counter; a wave's own step count would drift out of phase with the other
+// wave's) lets both progress at the same rate.
+__device__ __forceinline__ uint32_t simd_wave_slot() {
+  return __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11));   // HW_ID.WAVE_ID
+}
+__device__ __forceinline__ void fair_prio(uint32_t phase) {
+  if (phase & 1u) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
+// Probe build only (-DPBH_PHASES, scripts/phase_probe.sh): per-wave
+// real-time stamps (100 MHz) at the FULL pair kernel's phase boundaries.
+#ifdef PBH_PHASES
+#define PBH_PHASE_DECL uint64_t pbh_tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PBH_PHASE(k) (pbh_tph[k] = __builtin_amdgcn_s_memrealtime())
+// the loop's quarter points (i of n iterations) into words 5, 6, 7
+#define PBH_PHASE_Q(i, n)                                                     \
+  do {                                                                        \
+    if ((i) == (n) / 4) PBH_PHASE(5);                                         \
+    if ((i) == (n) / 2) PBH_PHASE(6);                                         \
+    if ((i) == 3 * (n) / 4) PBH_PHASE(7);                                     \
+  } while (0)
+// lane 0 of each wave writes its stamps, HW_ID and XCC_ID (8 words per wave)
+#define PBH_PHASE_STORE(buf, wave, lane)                                      \
+  do {                                                                        \
+    if ((lane) == 0 && (buf)) {                                               \
+      uint64_t *pb_ = reinterpret_cast<uint64_t *>(const_cast<double *>(buf)) \
+                      + (wave) * 8;                                           \
+      for (int k_ = 0; k_ < 8; ++k_) pb_[k_] = pbh_tph[k_];                   \
+      pb_[4] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));          \
+    }                                                                         \
+  } while (0)
+#else
+#define PBH_PHASE_DECL
+#define PBH_PHASE(k) ((void)0)
+#define PBH_PHASE_Q(i, n) ((void)0)
+#define PBH_PHASE_STORE(buf, wave, lane) ((void)0)
+#endif
+
 constexpr int kBm64LogN = 1025, kBm64ScN = 1024, kExp2N = 64;
 // layout in doubles: sin/cos words [0, 2048), log rows [2048, 4098), exp2
 constexpr int kBm64LogOff = 2 * kBm64ScN;                  // {-2 ln c, 1/c} rows

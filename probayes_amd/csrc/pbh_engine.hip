@@ -79,6 +79,7 @@ struct pbh_engine {
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
+  bool fair = true;          // PBH_FAIR=0: no wave-priority alternation
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -212,6 +213,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
+  if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::atoi(fa) != 0;
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
@@ -852,6 +854,22 @@ int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug
   return PBH_OK;
 }
 
+#ifdef PBH_PHASES
+// Probe build only: per-wave phase stamps of the last FULL pair launch
+// (8 words per wave; pbh_kernels_impl.h PBH_PHASE).
+static double *phase_buffer() {
+  static double *buf = nullptr;
+  if (!buf && hipMalloc(&buf, 4 << 20) == hipSuccess) hipMemset(buf, 0, 4 << 20);
+  return buf;
+}
+extern "C" int pbh_phase_dump(uint64_t *dst, int64_t words) {
+  if (words > (4 << 20) / 8) return PBH_ERR_ARG;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(dst, phase_buffer(), words * 8, hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+#endif
+
 int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   // PBH_TRACE_ENQUEUE=1: the host time of each enqueue phase to stderr
@@ -907,6 +925,9 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.seed_lo = (uint32_t)e->seed;
   k.seed_hi = (uint32_t)(e->seed >> 32);
   k.rep = e->rep;
+#ifdef PBH_PHASES
+  if (!k.rep) k.rep = phase_buffer();   // probe build: the FULL kernel's stamps
+#endif
   k.xo = e->xo;
   k.tx = e->tx; k.tlp = e->tlp; k.tpx = e->tpx; k.tpp = e->tpp; k.ts = e->ts;
   k.tacc = e->tacc;
@@ -938,6 +959,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gmm_full = e->gmm_full ? 1 : 0;
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
+  k.fair = e->fair ? 1 : 0;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;

@@ -120,6 +120,7 @@ struct KArgs {
   int32_t gmm_full;    // the quad kernel's steady-state form is allowed
   int32_t pair_full;   // the lane-pair kernel's steady-state form is allowed
   int32_t iid_full;    // cfg1's steady-state iid-Normal form is allowed
+  int32_t fair;        // alternate the SIMD's wave priorities (fair_prio)
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;

@@ -1114,6 +1114,8 @@ void mh_pair_kernel(KArgs a) {
   constexpr bool TAB = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_XOSHIRO;
   using PD = PairDraw<H, RNG>;
   __shared__ double s_bmt[TAB ? kBm64Doubles : 2];
+  PBH_PHASE_DECL;
+  PBH_PHASE(0);
   const bool lin = a.pscale == PBH_PSCALE_LIN;
   constexpr bool mom = MOM;   // running moments compiled in or out
   const int lane = threadIdx.x & 63;
@@ -1175,6 +1177,7 @@ void mh_pair_kernel(KArgs a) {
   // Drain the entry loads here: a wait for them inside the loop would also
   // wait for every trace store issued before it.
   __builtin_amdgcn_s_waitcnt(0);
+  PBH_PHASE(1);
 
   // One chain-step.  (r, t0, t1) are this step's draws (Philox: supplied by
   // the caller, t0 = the LB-bit threshold lead).
@@ -1459,7 +1462,11 @@ void mh_pair_kernel(KArgs a) {
           normals(w, I0{}, IH{}, cA, cB);
           ctA = w[3 * H] >> 16;
           ctB = w[3 * H] & 0xFFFFu;
+          PBH_PHASE(2);
+          const uint32_t slot = a.fair ? simd_wave_slot() : 0u;
           for (; s + 3 < a.n_steps; s += 2) {
+            if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 7) + slot);
+            PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
             uint32_t nw[4 * NB];
             double nA[H], nB[H];
             philox(((a.g0 + s) >> 1) + 1, nw);
@@ -1485,6 +1492,7 @@ void mh_pair_kernel(KArgs a) {
           normals(w, I0{}, IA{}, cA, cB);
           step_full(s, cA, w[3 * H] >> 16);
         }
+        PBH_PHASE(3);
     } else {
       if (a.g0 & 1) {   // launch starts on a pair's 2nd step
         PD::draw(a, s_bmt, h, a.g0 >> 1, chain, cA, cB, ctA, ctB);
@@ -1520,6 +1528,10 @@ void mh_pair_kernel(KArgs a) {
       if (hi) a.nacc[c] += nacc;
     }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, h, c, xs);
+  }
+  if constexpr (FULL) {   // probe build only (a.rep is the phase buffer)
+    PBH_PHASE(4);
+    PBH_PHASE_STORE(a.rep, wave, lane);
   }
 }
 // ---------------------------------------------------------------------------
@@ -1906,6 +1918,8 @@ void mh_gmm_quad_kernel(KArgs a) {
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
   constexpr int LB = kStepLead;          // threshold lead bits (step_draws)
   __shared__ double s_bmt[kBm64Doubles];
+  PBH_PHASE_DECL;
+  PBH_PHASE(0);
   const int lane = threadIdx.x & 63;
   const int p = lane & 3;
   const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1943,6 +1957,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   const int64_t rstride = (int64_t)D * a.n;
   bm64_load(s_bmt, a.bm64);        // after the state's loads: all in flight
   __builtin_amdgcn_s_waitcnt(0);   // entry loads drained before the loop
+  PBH_PHASE(1);
 
   const int64_t gend = a.g0 + a.n_steps;
   uint64_t inlm = __ballot(__builtin_fabs(lm) <= 698.);   // FULL: |lm| <= 698
@@ -1959,7 +1974,11 @@ void mh_gmm_quad_kernel(KArgs a) {
   double rnext[D];
   uint32_t lnext = 0;
   if constexpr (FULL) lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
+  PBH_PHASE(2);
+  const uint32_t slot = FULL && a.fair ? simd_wave_slot() : 0u;
   for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
+    if (FULL && a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 7) + slot);
+    if constexpr (FULL) PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
     // ---- lane p draws step 4 G + p; the quad shares the group's draws
     double rown[D];
     uint32_t lown;
@@ -2175,6 +2194,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + cc]);
     }
   }
+  PBH_PHASE(3);
   if (active) {
     if (p < D) {
       double xo = x[0];
@@ -2190,6 +2210,10 @@ void mh_gmm_quad_kernel(KArgs a) {
       a.lp[c] = lm == lp0 && ls == 1.0 ? lp0 : lm + ln_tab(ls, s_bmt);
       if constexpr (MOM) a.nacc[c] += nacc;
     }
+  }
+  if constexpr (FULL) {   // probe build only (a.rep is the phase buffer)
+    PBH_PHASE(4);
+    PBH_PHASE_STORE(a.rep, wave, lane);
   }
 }
 // ---------------------------------------------------------------------------
