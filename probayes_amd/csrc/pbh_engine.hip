@@ -80,6 +80,8 @@ struct pbh_engine {
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
   bool fair = true;          // PBH_FAIR=0: no wave-priority alternation
+  int lockstep = 0;          // PBH_LOCKSTEP=k: FULL pair waves meet every k pairs
+  int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -214,6 +216,8 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::atoi(fa) != 0;
+  if (const char *ls = std::getenv("PBH_LOCKSTEP")) e->lockstep = std::max(0, std::atoi(ls));
+  if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
@@ -960,6 +964,8 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
   k.fair = e->fair ? 1 : 0;
+  k.lockstep = e->lockstep;
+  k.pair_wg = e->pair_wg;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;

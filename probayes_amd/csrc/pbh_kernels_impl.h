@@ -25,6 +25,7 @@ namespace pbh {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kPairFullBlock = 512;   // FULL pair kernel's largest workgroup
 
 // Model constants are never written by a kernel: reading them through the
 // constant address space lets the compiler use scalar loads (s_load) with
@@ -1103,7 +1104,8 @@ __device__ __attribute__((noinline)) bool pair_exact(uint32_t seed_lo, uint32_t 
 // chain).  The same words and arithmetic as the general form: identical
 // chains (tests/test_gpu_parity.py).
 template <int D, int RNG, bool MOM, bool LOC0 = false, bool FULL = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(FULL ? kPairFullBlock : kBlock)
+__attribute__((amdgpu_waves_per_eu(2)))
 void mh_pair_kernel(KArgs a) {
   static_assert(!FULL || (RNG == PBH_RNG_PHILOX && !MOM), "FULL: production Philox");
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
@@ -1121,7 +1123,8 @@ void mh_pair_kernel(KArgs a) {
   const int lane = threadIdx.x & 63;
   const bool hi = lane >= 32;
   const int h = hi ? 1 : 0;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave =
+      ((int64_t)blockIdx.x * (FULL ? (int)blockDim.x : kBlock) + threadIdx.x) >> 6;
   const int64_t c = wave * 32 + (lane & 31);
   const bool active = c < a.n;
   const int64_t cc = active ? c : 0;
@@ -1467,6 +1470,9 @@ void mh_pair_kernel(KArgs a) {
           for (; s + 3 < a.n_steps; s += 2) {
             if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 7) + slot);
             PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
+            // lockstep: the SIMD's two waves (one workgroup) meet every
+            // a.lockstep pairs (no memory fence: the stores stay in flight)
+            if (a.lockstep && ((s >> 1) % a.lockstep) == 0) __builtin_amdgcn_s_barrier();
             uint32_t nw[4 * NB];
             double nA[H], nB[H];
             philox(((a.g0 + s) >> 1) + 1, nw);
@@ -2852,6 +2858,12 @@ void launch_mh_pair_m(const KArgs &a, hipStream_t st, dim3 grid, dim3 block) {
 template <int D>
 void launch_mh_pair(const KArgs &a, hipStream_t st) {
   const int64_t waves = (a.n + 31) / 32;
+  if (!a.moments && pair_full_form(a)) {   // FULL: 4- or 8-wave workgroups
+    const int wg = a.pair_wg == kPairFullBlock ? kPairFullBlock : kBlock;
+    const dim3 grid((unsigned)((waves * 64 + wg - 1) / wg)), block(wg);
+    launch_mh_pair_m<D, false>(a, st, grid, block);
+    return;
+  }
   const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
   if (a.moments) launch_mh_pair_m<D, true>(a, st, grid, block);
   else launch_mh_pair_m<D, false>(a, st, grid, block);
