@@ -79,7 +79,7 @@ struct pbh_engine {
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
-  bool fair = true;          // PBH_FAIR=0: no wave-priority alternation
+  int fair = 7;              // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
   int lockstep = 0;          // PBH_LOCKSTEP=k: FULL pair waves meet every k pairs
   int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
   bool event_markers = true;
@@ -215,7 +215,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
-  if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::atoi(fa) != 0;
+  if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::min(20, std::max(0, std::atoi(fa)));
   if (const char *ls = std::getenv("PBH_LOCKSTEP")) e->lockstep = std::max(0, std::atoi(ls));
   if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
@@ -963,7 +963,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gmm_full = e->gmm_full ? 1 : 0;
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
-  k.fair = e->fair ? 1 : 0;
+  k.fair = e->fair;
   k.lockstep = e->lockstep;
   k.pair_wg = e->pair_wg;
   k.gq = e->gq;

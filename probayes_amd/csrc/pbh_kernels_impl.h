@@ -1468,7 +1468,7 @@ void mh_pair_kernel(KArgs a) {
           PBH_PHASE(2);
           const uint32_t slot = a.fair ? simd_wave_slot() : 0u;
           for (; s + 3 < a.n_steps; s += 2) {
-            if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 7) + slot);
+            if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
             PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
             // lockstep: the SIMD's two waves (one workgroup) meet every
             // a.lockstep pairs (no memory fence: the stores stay in flight)
@@ -1983,7 +1983,7 @@ void mh_gmm_quad_kernel(KArgs a) {
   PBH_PHASE(2);
   const uint32_t slot = FULL && a.fair ? simd_wave_slot() : 0u;
   for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
-    if (FULL && a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 7) + slot);
+    if (FULL && a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
     if constexpr (FULL) PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
     // ---- lane p draws step 4 G + p; the quad shares the group's draws
     double rown[D];
