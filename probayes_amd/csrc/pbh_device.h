@@ -297,7 +297,11 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 // (profiles/r03_phase_*, scripts/phase_probe.py).  Alternating the priority
 // between the SIMD's two wave slots on a shared clock (the 100 MHz real-time
 // counter; a wave's own step count would drift out of phase with the other
-// wave's) lets both progress at the same rate.
+// wave's) every ~20 us (PBH_FAIR=11, the engine's default) hands the lead
+// back and forth, so both end together: cfg2 250-step launches 0.59 -> 0.63
+// of HBM, cfg5's quad kernel 1 071 -> 956 us.  Short periods (1.3 us) and
+// workgroup barriers keep the waves in phase and lose the leader / filler
+// interleave (r03_phase_quarters.txt).
 __device__ __forceinline__ uint32_t simd_wave_slot() {
   return __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11));   // HW_ID.WAVE_ID
 }

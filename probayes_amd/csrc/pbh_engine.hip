@@ -79,7 +79,7 @@ struct pbh_engine {
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
-  int fair = 7;              // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
+  int fair = 11;             // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
   int lockstep = 0;          // PBH_LOCKSTEP=k: FULL pair waves meet every k pairs
   int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
   bool event_markers = true;
