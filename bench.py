@@ -22,6 +22,7 @@ and ONE RCCL all-gather collects the per-chain statistics (timed separately).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -103,22 +104,30 @@ def _cgroup_cpus():
     return None
 
 
+def cpu_cores():
+  """The CPUs this process may actually run on: the affinity mask, capped by
+  the cgroup quota (a 16-CPU quota over a 256-CPU mask is 16 CPUs of time)."""
+  mask, ncpu = _cpu_mask()
+  quota = _cgroup_cpus()
+  cores = ncpu if quota is None else max(1, min(ncpu, int(math.ceil(quota))))
+  return cores, mask, ncpu, quota
+
+
 def cpu_baseline(budget_s=6.0, chains=65536):
   """cfg2 on this host's cores, timed BEFORE the GPU is touched (the worker
   processes are forked from a process with no HIP state): the vectorised
   NumPy restatement (oracle/vector_mh.py, the reference's per-step arithmetic
   for all chains at once, every step recorded) at N = 65 536 on one core,
-  then split over one process per CPU of the affinity mask (the
-  split across all host cores, mask stated).  The reference SP itself: 877
-  chain-steps/s on 1 core."""
+  then split over one process per usable CPU (cpu_cores: the affinity mask
+  capped by the cgroup quota, so `cores` is what the processes really ran
+  on).  The reference SP itself: 877 chain-steps/s on 1 core."""
   import multiprocessing as mp
   t = 16
   one_done, one_el = _cpu_slice((chains, t, budget_s, 1))
-  mask, ncpu = _cpu_mask()
-  quota = _cgroup_cpus()
-  procs = max(1, min(ncpu, 1000))   # the box allows 1024 processes
+  cores, mask, ncpu, quota = cpu_cores()
+  procs = min(cores, 1000)   # the box allows 1024 processes
   # independent chains per process; at least 4096 so that each process's
-  # vectorised steps stay efficient when the mask is wide
+  # vectorised steps stay efficient when there are many
   per = max(-(-chains // procs), 4096)
   ctx = mp.get_context('fork')
   with ctx.Pool(procs) as pool:
@@ -127,18 +136,19 @@ def cpu_baseline(budget_s=6.0, chains=65536):
   return {'value': rate_all, 'unit': 'chain-steps/s', 'cores': procs,
           'kind': 'port',
           'single_core': one_done / one_el,
-          'affinity': mask, 'cgroup_cpu_quota': quota,
+          'affinity': mask, 'affinity_cpus': ncpu, 'cgroup_cpu_quota': quota,
           'reference_sp_1core': 877.0,
           'sample': 'cfg2 (d = 10), oracle/vector_mh.py vectorised NumPy '
                     'restatement, every step recorded: {} chains x {}-step '
                     'runs for {:.0f} s on 1 core ({:.3g} chain-steps/s), then '
-                    '{} processes (one per CPU of the affinity mask {}; cgroup '
-                    'quota {} CPUs) x {} chains for {:.0f} s each; the '
+                    '{} processes (affinity mask {} = {} CPUs, cgroup quota {} '
+                    'CPUs: {} usable) x {} chains for {:.0f} s each; the '
                     'reference SP: 877 chain-steps/s on 1 core '
                     '(BASELINE.md)'.format(chains, t, budget_s,
                                            one_done / one_el, procs, mask,
+                                           ncpu,
                                            quota if quota else 'unlimited',
-                                           per, budget_s)}
+                                           cores, per, budget_s)}
 
 
 def measured_traffic(chains, launch_steps, rng, trace):
@@ -264,9 +274,11 @@ def main():
   if world != args.gpus:
     raise SystemExit('--gpus {} but WORLD_SIZE {}'.format(args.gpus, world))
 
-  # the CPU baseline runs first, before anything touches the GPU
+  # the CPU baseline runs first on rank 0, before anything touches its GPU;
+  # at world > 1 the other ranks wait for it at the ncclUniqueId hand-off
+  # (exchange_unique_id), so every SCALE line carries the baseline too
   cpu = None
-  if world == 1 and rank == 0 and not args.no_cpu_baseline:
+  if rank == 0 and not args.no_cpu_baseline:
     cpu = cpu_baseline()
 
   from probayes_amd import Engine

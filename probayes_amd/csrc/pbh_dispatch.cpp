@@ -486,10 +486,15 @@ __global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
     xa[q] = 0.;
     xb[q] = 0.;
     if (t < T) {
-      if (has_b) {
+      if (has_b && !(row & 1)) {
+        // series s0, s0 + 1: adjacent doubles, 16-byte aligned when the
+        // record length d n is even (s0 is even, the trace base aligned)
         const double2 v = *reinterpret_cast<const double2 *>(src + (int64_t)t * row);
         xa[q] = v.x;
         xb[q] = v.y;
+      } else if (has_b) {   // odd d n: every other record is 8-byte aligned
+        xa[q] = src[(int64_t)t * row];
+        xb[q] = src[(int64_t)t * row + 1];
       } else {
         xa[q] = src[(int64_t)t * row];
       }

@@ -80,7 +80,6 @@ struct pbh_engine {
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
   int fair = 11;             // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
-  int lockstep = 0;          // PBH_LOCKSTEP=k: FULL pair waves meet every k pairs
   int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
@@ -216,7 +215,6 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::min(20, std::max(0, std::atoi(fa)));
-  if (const char *ls = std::getenv("PBH_LOCKSTEP")) e->lockstep = std::max(0, std::atoi(ls));
   if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
@@ -964,7 +962,6 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
   k.fair = e->fair;
-  k.lockstep = e->lockstep;
   k.pair_wg = e->pair_wg;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
@@ -1367,16 +1364,30 @@ int pbh_rccl_init(pbh_engine *e, int32_t rank, int32_t world, const uint8_t id[1
 namespace {
 
 // Every rank enters every collective of a gather, whatever failed locally: a
-// rank that cannot proceed votes NaN in an all-reduce of (status, count) and
-// every rank then returns the same error -- no rank is left waiting inside
-// RCCL (a collective only some ranks enter never completes).  Local HIP
-// failures between two agreements are not returned on the spot: they become
-// the rank's vote at the next agreement, which every rank enters.
+// rank that cannot proceed votes a positive status in an all-reduce of
+// (status, count, -count) under ncclMax -- 0 = ok, rank + 1 = this rank
+// failed -- and every rank then returns the same error: no rank is left
+// waiting inside RCCL (a collective only some ranks enter never completes).
+// The vote is a finite number on purpose: a float max may drop a NaN operand
+// depending on the operand order (fmax, compare-select), so a NaN vote could
+// vanish at world >= 2; a positive status survives any max.  When the vote
+// cannot be copied to the device, the fallback fills the whole vote with
+// 0x3F bytes (4.8e-4 per double: still positive, so still "failed").  Local
+// HIP failures between two agreements are not returned on the spot: they
+// become the rank's vote at the next agreement, which every rank enters.
+constexpr unsigned char kFailFill = 0x3F;   // 0x3F3F...3F = 4.8e-4 > 0
+
+int vote_failure(const char *what, double status) {
+  if (status >= 1.)
+    return fail(PBH_ERR_STATE, "%s: rank %d could not take part (the highest failing "
+                "rank; see its own error)", what, (int)status - 1);
+  return fail(PBH_ERR_STATE, "%s: a rank could not take part (see its own error)", what);
+}
+
 int rccl_agree(pbh_engine *e, bool ok, int64_t n, int64_t *n_max, const char *what) {
-  double v[3] = {ok ? 0. : std::nan(""), (double)n, -(double)n};
+  double v[3] = {ok ? 0. : (double)(e->rank + 1), (double)n, -(double)n};
   hipError_t h = hipMemcpy(e->scalar, v, sizeof v, hipMemcpyHostToDevice);
-  if (h != hipSuccess)   // the vote must still say "failed": all-ones is a NaN
-    (void)hipMemset(e->scalar, 0xFF, sizeof(double));
+  if (h != hipSuccess) (void)hipMemset(e->scalar, kFailFill, sizeof v);
   // the collective is entered whatever happened above
   const ncclResult_t r = ncclAllReduce(e->scalar, e->scalar, 3, ncclFloat64, ncclMax,
                                        e->comm, e->stream);
@@ -1386,8 +1397,7 @@ int rccl_agree(pbh_engine *e, bool ok, int64_t n, int64_t *n_max, const char *wh
     return fail(PBH_ERR_RCCL, "%s: %s", what, ncclGetErrorString(r));
   if (h != hipSuccess || s != hipSuccess)
     return fail(PBH_ERR_HIP, "%s: %s", what, hipGetErrorString(h != hipSuccess ? h : s));
-  if (v[0] != v[0])
-    return fail(PBH_ERR_STATE, "%s: a rank could not take part (see its own error)", what);
+  if (!(v[0] == 0.)) return vote_failure(what, v[0]);
   if (n_max) *n_max = (int64_t)v[1];
   return PBH_OK;
 }
@@ -1477,22 +1487,24 @@ int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
 int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
   if (check_ptr(e, "engine") || check_ptr(value, "value")) return PBH_ERR_ARG;
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
-  double v = *value;
+  // (value, status): the status is rccl_agree's finite vote
+  double v[2] = {*value, 0.};
   hipError_t h = hipSetDevice(e->device);
-  h = keep(h, hipMemcpy(e->scalar, &v, sizeof(double), hipMemcpyHostToDevice));
-  if (h != hipSuccess) (void)hipMemset(e->scalar, 0xFF, sizeof(double));   // NaN: failed
-  // entered whatever happened above (a NaN max tells every rank)
-  const ncclResult_t r = ncclAllReduce(e->scalar, e->scalar, 1, ncclFloat64, ncclMax,
+  if (h != hipSuccess) v[1] = (double)(e->rank + 1);
+  h = keep(h, hipMemcpy(e->scalar, v, sizeof v, hipMemcpyHostToDevice));
+  if (h != hipSuccess) (void)hipMemset(e->scalar, kFailFill, sizeof v);
+  // entered whatever happened above (a positive status tells every rank)
+  const ncclResult_t r = ncclAllReduce(e->scalar, e->scalar, 2, ncclFloat64, ncclMax,
                                        e->comm, e->stream);
   hipError_t s = hipStreamSynchronize(e->stream);
-  if (s == hipSuccess) s = hipMemcpy(&v, e->scalar, sizeof(double), hipMemcpyDeviceToHost);
+  if (s == hipSuccess) s = hipMemcpy(v, e->scalar, sizeof v, hipMemcpyDeviceToHost);
   if (r != ncclSuccess) return fail(PBH_ERR_RCCL, "pbh_rccl_allreduce_max: %s",
                                     ncclGetErrorString(r));
   if (h != hipSuccess || s != hipSuccess)
     return fail(PBH_ERR_HIP, "pbh_rccl_allreduce_max: %s",
                 hipGetErrorString(h != hipSuccess ? h : s));
-  if (v != v) return fail(PBH_ERR_STATE, "pbh_rccl_allreduce_max: a rank failed");
-  *value = v;
+  if (!(v[1] == 0.)) return vote_failure("pbh_rccl_allreduce_max", v[1]);
+  *value = v[0];
   return PBH_OK;
 }
 

@@ -121,7 +121,6 @@ struct KArgs {
   int32_t pair_full;   // the lane-pair kernel's steady-state form is allowed
   int32_t iid_full;    // cfg1's steady-state iid-Normal form is allowed
   int32_t fair;        // alternate the SIMD's wave priorities every 2^fair real-time ticks (0: off)
-  int32_t lockstep;    // FULL pair kernel: workgroup barrier every k pairs (0: none)
   int32_t pair_wg;     // FULL pair kernel's workgroup size (256 or 512)
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)

@@ -1470,9 +1470,6 @@ void mh_pair_kernel(KArgs a) {
           for (; s + 3 < a.n_steps; s += 2) {
             if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
             PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
-            // lockstep: the SIMD's two waves (one workgroup) meet every
-            // a.lockstep pairs (no memory fence: the stores stay in flight)
-            if (a.lockstep && ((s >> 1) % a.lockstep) == 0) __builtin_amdgcn_s_barrier();
             uint32_t nw[4 * NB];
             double nA[H], nB[H];
             philox(((a.g0 + s) >> 1) + 1, nw);

@@ -94,6 +94,14 @@ def fault_at(rank, step):
   return int(r) == rank and int(st or 3) == step
 
 
+def vote_message(what, status):
+  """The error of a failed agreement (pbh_engine.hip vote_failure)."""
+  if status >= 1:
+    return ('{}: rank {} could not take part (the highest failing rank; see its '
+            'own error)'.format(what, int(status) - 1))
+  return '{}: a rank could not take part (see its own error)'.format(what)
+
+
 class TcpCollective:
   """Star-topology exchange over TCP: rank 0 listens on (addr, port), the
   other ranks connect and announce their rank.  Used for the ncclUniqueId
@@ -169,33 +177,54 @@ class TcpCollective:
       pos += 8 + n
     return np.stack(out)
 
-  def allreduce_max(self, value):
-    return float(self.allgather(np.array([float(value)])).max())
+  @staticmethod
+  def _max(votes):
+    """Elementwise max over ranks with NaN-DROPPING semantics (np.fmax): the
+    operand-order-dependent behaviour a float max may have inside RCCL.  The
+    votes are finite by construction, so the result does not depend on it."""
+    return np.fmax.reduce(np.asarray(votes, np.float64), axis=0)
+
+  def allreduce_max(self, value, ok=True):
+    """pbh_rccl_allreduce_max: (value, status) under one max; a positive
+    status (rank + 1 of a failed rank) makes every rank raise."""
+    v = self._max(self.allgather(np.array([float(value),
+                                           0. if ok else self.rank + 1.])))
+    if v[1] != 0:
+      raise CollectiveError(vote_message('allreduce_max', v[1]))
+    return float(v[0])
 
   def agree(self, ok, n, what):
-    """pbh_engine's rccl_agree: every rank votes (status, count); a rank
-    that failed locally votes NaN and every rank raises the same error."""
-    v = self.allgather(np.array([0. if ok else np.nan, float(n)]))
-    if np.isnan(v[:, 0]).any():
-      raise CollectiveError('{}: rank(s) {} could not take part'.format(
-          what, [int(r) for r in np.flatnonzero(np.isnan(v[:, 0]))]))
-    return v[:, 1].astype(np.int64)
+    """pbh_engine's rccl_agree: every rank votes (status, n, -n) -- status 0
+    = ok, rank + 1 = this rank failed locally -- combined by one elementwise
+    max; any positive status makes every rank raise the same error.
+    Returns the largest n (the gather's padded width)."""
+    v = self._max(self.allgather(
+        np.array([0. if ok else self.rank + 1., float(n), -float(n)])))
+    if v[0] != 0:
+      raise CollectiveError(vote_message(what, v[0]))
+    return int(v[1])
 
   def allgather_stats(self, sum_, sumsq, n_acc, ess=None):
-    """The engine's pbh_rccl_allgather_stats contract on the CPU: the
-    padded [world][3d+1][n_max] block and every rank's count, behind the same
-    agreements (chains, buffers, packing; PBH_FAULT_GATHER injects a local
-    failure) so that a failing rank makes every rank fail, none wait."""
+    """The engine's pbh_rccl_allgather_stats contract on the CPU: agree on
+    the padded width, then the [world][3d+2][n_max] all-gather whose last row
+    carries each rank's count (element 0), behind the same agreements
+    (chains, buffers, packing; PBH_FAULT_GATHER injects a local failure) so
+    that a failing rank makes every rank fail, none wait.  Returns the
+    [world][3d+1][n_max] statistics block and the counts."""
     n = np.asarray(sum_).shape[0]
-    counts = self.agree(not fault_at(self.rank, 1), n, 'allgather_stats')
+    n_max = self.agree(not fault_at(self.rank, 1), n, 'allgather_stats')
     self.agree(not fault_at(self.rank, 2), n, 'allgather_stats (buffers)')
     ok = not fault_at(self.rank, 3)
     try:
-      blk = pack_stats(sum_, sumsq, n_acc, ess, n_max=int(counts.max()))
+      blk = pack_stats(sum_, sumsq, n_acc, ess, n_max=n_max)
+      cnt = np.zeros((1, n_max))
+      cnt[0, 0] = n
+      blk = np.concatenate([blk, cnt])
     except Exception:   # this rank's failure is its vote
       ok, blk = False, None
     self.agree(ok, n, 'allgather_stats (packing)')
-    return self.allgather(blk), counts
+    got = self.allgather(blk)
+    return got[:, :-1], got[:, -1, 0].astype(np.int64)
 
   def close(self):
     for conn in self.peers.values():

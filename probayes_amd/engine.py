@@ -333,10 +333,27 @@ class Engine:
       raise ValueError('checkpoint shape does not match the engine')
     xo = ck.get('xo')
     xo = None if xo is None else np.ascontiguousarray(xo, np.uint32)
+    if xo is not None and xo.size != 8 * self.n:   # [4 words][2 halves][N]
+      raise ValueError('checkpoint xoshiro state has {} words, the engine needs '
+                       '{}'.format(xo.size, 8 * self.n))
+    mt = ck.get('mt')
+    if mt is not None:
+      # the C side copies words x N, N, N, N values from these arrays: a
+      # checkpoint of the other legacy layout (PBH_LEGACY_DB) or of another
+      # chain count would be read past its end
+      words = _c.c_int64()
+      _lib.call('pbh_legacy_state_words', self._h, _c.byref(words))
+      want = {'key': (words.value, self.n), 'pos': (self.n,), 'has': (self.n,),
+              'gauss': (self.n,)}
+      for k, shape in want.items():
+        got = np.shape(mt[k])
+        if got != shape:
+          raise ValueError('checkpoint legacy state {} has shape {}, this engine '
+                           'needs {} (legacy layout words per chain: {})'.format(
+                               k, got, shape, words.value))
     _lib.call('pbh_restore', self._h, _dp(x), _dp(lp),
               _c.c_int64(int(ck['step'])), 1 if ck['has_pred'] else 0,
               None if xo is None else xo.ctypes.data_as(_lib._u32p))
-    mt = ck.get('mt')
     if mt is not None:   # device legacy streams continue where they were
       key = np.ascontiguousarray(mt['key'], np.uint32)
       pos = np.ascontiguousarray(mt['pos'], np.int32)

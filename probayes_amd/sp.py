@@ -17,6 +17,7 @@ Extensions over the reference (keyword-only, defaults keep its behaviour):
   device=, thin=, steps_per_launch=.
 """
 import collections
+import weakref
 import warnings
 
 import numpy as np
@@ -493,9 +494,9 @@ class SP:
     if self._samplers is None or sampler_id is None:
       self._samplers = []
     if self._counter is None:
-      self._counter = collections.Counter()
+      self._counter = _WeakCounter()
     if self._last is None:
-      self._last = collections.OrderedDict()
+      self._last = weakref.WeakKeyDictionary()
     if sampler_id is None:
       return None
     sampler = self.get_sampler(sampler_id)
@@ -593,6 +594,16 @@ class SP:
         if pd is not None:
           summary = summary._replace(**{key: pd.conditionalise(list(pd.keys()))})
     return summary
+
+
+class _WeakCounter(weakref.WeakKeyDictionary):
+  """SP's step counters (sp.py:113-128: a collections.Counter keyed by
+  sampler) without keeping the samplers alive: a sampler dropped by the
+  caller and by SP.reset()'s registry is collected, and with it its engine's
+  device buffers.  Missing samplers count 0, as in a Counter."""
+
+  def __getitem__(self, key):
+    return self.data.get(weakref.ref(key), 0)
 
 
 OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',
@@ -734,7 +745,12 @@ class Sampler:
     self._epoch = True      # the next step starts an epoch (at init)
     self._drawn = []        # (global step, steps) drawn from seeded streams
     self._done = False      # a bounded sampler ran out (sp_utils.py:14-16)
-    self.blocks = []
+    # global-stream draw-ahead (rng 'legacy', seeds None): steps computed
+    # ahead per block; back to one step after a caller's own draw forced a
+    # rewind, doubled per block after that (interleaved samplers cost O(1)
+    # per step instead of a redraw of the whole remaining stop)
+    self._ahead = self.chunk
+    self.n_computed = 0     # chain-steps' worth of steps run (diagnostic)
 
   def __repr__(self):
     return '<probayes_amd Sampler {} stop={}>'.format(self.sid, self.stop)
@@ -840,12 +856,18 @@ class Sampler:
       pass
 
   # ---- computing blocks ----------------------------------------------------
+  def _global_stream(self):
+    return self.rng == 'legacy' and self.seeds is None
+
   def _block_steps(self):
+    k = self.chunk
     if self.stop is not None:
       left = self.stop - self.sp.get_counter(self)
       if left > 0:
-        return left - left % self.thin if left >= self.thin else self.thin
-    return self.chunk
+        k = left - left % self.thin if left >= self.thin else self.thin
+    if self._global_stream():
+      k = min(k, self._ahead)
+    return k
 
   def _draw_global(self, k):
     """k steps of the single chain's legacy stream from NumPy's global
@@ -874,9 +896,11 @@ class Sampler:
     else:
       tr, thr, prev_x, prev_p = self._compute_engine(k, rewind)
     self._g = g0 + k
-    b = _Block(tr, thr, prev_x, prev_p, first, g0, rewind)
-    self.blocks.append(b)
-    self._cur, self._j = b, 0
+    self.n_computed += k
+    if self._global_stream():
+      self._ahead = min(2 * self._ahead, 1 << 30)
+    # Steps keep their own block; the sampler keeps only the current one
+    self._cur, self._j = _Block(tr, thr, prev_x, prev_p, first, g0, rewind), 0
 
   def _compute_engine(self, k, rewind):
     eng = self._eng
@@ -973,6 +997,7 @@ class Sampler:
       # someone drew from the global stream since the last step: the steps
       # drawn ahead are not the reference's any more
       self._rewind_to_handed()
+      self._ahead = self.thin
       cur = None
     if cur is None or self._j >= cur.T:
       self._compute()
@@ -981,6 +1006,8 @@ class Sampler:
     self._j += 1
     if 'states' in cur.rewind:
       np.random.set_state(cur.rewind['states'][(j + 1) * self.thin - 1])
+      if self._j >= cur.T:   # fully handed out: no rewind into it any more
+        del cur.rewind['states']
     self._handed = (cur, j)
     if self._is_gibbs():   # the RF's __cond_mod follows the steps handed out
       self._cycle_rf()._pbh_cond_step = \

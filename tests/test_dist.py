@@ -239,7 +239,7 @@ try:
   col.allgather_stats(s, s, np.zeros(n))
   print('NO_ERROR', rank)
 except CollectiveError as e:
-  assert '[1]' in str(e), str(e)
+  assert 'rank 1 could not take part' in str(e), str(e)
   # the protocol stays in step after a failure: the next collective works
   assert col.allreduce_max(rank) == world - 1
   print('FAILED_AS_ONE', rank)
@@ -257,3 +257,22 @@ def test_a_rank_failing_inside_the_gather_fails_every_rank(tmp_path, monkeypatch
   script.write_text(FAULT_WORKER.format(root=ROOT))
   outs = _spawn(script, 2, _free_port())
   assert 'FAILED_AS_ONE 0' in outs[0] and 'FAILED_AS_ONE 1' in outs[1], outs
+
+
+def test_failure_vote_survives_a_nan_dropping_max():
+  """a NaN vote can vanish under a float max that drops
+  NaN operands (fmax / compare-select, operand-order dependent); the vote is
+  therefore a finite status (0 ok, rank + 1 failed), which every max keeps.
+  The TCP stand-in reduces with np.fmax, the adversarial semantics."""
+  from probayes_amd.dist import vote_message
+  nan_votes = np.array([[0., 5., -5.], [np.nan, 4., -4.]])
+  assert TcpCollective._max(nan_votes)[0] == 0.    # the old vote is lost
+  for order in ([0, 1, 2], [2, 1, 0], [1, 0, 2]):
+    votes = np.array([[0., 5., -5.], [2., 4., -4.], [0., 3., -3.]])[order]
+    red = TcpCollective._max(votes)
+    assert red[0] == 2. and red[1] == 5.
+    assert 'rank 1 could not take part' in vote_message('x', red[0])
+  # the engine's fallback fill (0x3F bytes) is a positive finite double
+  fill = np.frombuffer(bytes([0x3F]) * 8, np.float64)[0]
+  assert np.isfinite(fill) and 0. < fill < 1.
+  assert 'a rank could not take part' in vote_message('x', fill)

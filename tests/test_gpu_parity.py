@@ -259,7 +259,10 @@ def _ess_ips(x):
 @pytest.mark.parametrize('fft', ['1', '0'])
 @pytest.mark.parametrize('name,n,t,burn', [('gmm2', 2000, 600, 100),
                                            ('diag10', 300, 257, 7),
-                                           ('gmm2', 33, 2100, 40)])
+                                           ('gmm2', 33, 2100, 40),
+                                           # odd d n: unaligned series pairs
+                                           ('mcmc_prob2', 33, 300, 10),
+                                           ('bound_list3', 33, 300, 10)])
 def test_device_ess_and_trace_stats_match_host(monkeypatch, name, n, t, burn, fft):
   """pbh_trace_ess (on-device initial positive sequence: the FFT kernel,
   or with PBH_ESS_FFT=0 the direct-sum kernel; more than 2 048 records
@@ -642,3 +645,50 @@ def test_checkpoint_resume_continues_the_run(name, rng):
     assert _rel_err(got['v_p'], ref['v_p'][:, t1:]) <= 1e-9
   else:
     assert np.array_equal(got['v_p'], ref['v_p'][:, t1:])
+
+
+def test_checkpoint_with_device_legacy_streams_and_shape_checks():
+  """The legacy-stream part of a checkpoint (MT19937 key, position, cached
+  gauss): a fresh engine seeded the same way and restored continues the
+  uninterrupted reference-identical run; a checkpoint whose legacy state does
+  not match the engine's layout or chain count is refused before any copy
+  (the C side copies words x N values from the arrays)."""
+  from probayes_amd import Engine
+  name = 'diag10'
+  spec = oracle.golden_spec(name)
+  n, t, t1 = 300, 30, 11
+  seeds = 1000 + np.arange(n)
+
+  def engine():
+    e = Engine(spec)
+    e.init_chains(golden_init(name, n))
+    e.set_rng('replay')
+    e.seed_legacy(seeds)
+    return e
+  full = engine()
+  full.legacy_replay(t)
+  full.alloc_trace(t, 1)
+  full.run(t)
+  ref = full.trace()
+  full.close()
+  a = engine()
+  a.legacy_replay(t1)
+  a.run(t1)
+  ck = a.checkpoint()
+  a.close()
+  assert ck['mt'] is not None
+  b = engine()
+  for bad in ({'key': ck['mt']['key'][:624]}, {'pos': ck['mt']['pos'][:-1]},
+              {'gauss': np.zeros(n + 1)}):
+    with pytest.raises(ValueError, match='legacy state'):
+      b.restore(dict(ck, mt=dict(ck['mt'], **bad)))
+  with pytest.raises(ValueError, match='xoshiro'):
+    b.restore(dict(ck, xo=np.zeros(5, np.uint32)))
+  b.restore(ck)
+  b.legacy_replay(t - t1)
+  b.alloc_trace(t - t1, 1)
+  b.run(t - t1)
+  got = b.trace()
+  b.close()
+  assert np.array_equal(got['u'], ref['u'][:, t1:])
+  assert np.array_equal(got['v_x'], ref['v_x'][:, t1:])

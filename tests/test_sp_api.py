@@ -201,3 +201,54 @@ def test_summary_spans_blocks():
     np.testing.assert_array_equal(np.asarray(a.o[key]), np.asarray(b.o[key]))
     np.testing.assert_array_equal(np.asarray(a.p[key]), np.asarray(b.p[key]))
   assert a.u == b.u
+
+
+@pytest.mark.gpu
+def test_interleaved_bounded_samplers_cost_linear_draw_ahead():
+  """two bounded samplers on the global stream, stepped in
+  turn.  Each one's draws interleave with the other's in NumPy's global
+  state, so every step of one invalidates what the other drew ahead; the
+  draw-ahead falls back to one step after such a rewind (then doubles), so
+  the steps computed stay O(stop) per sampler, and both chains equal the
+  oracle fed the same interleaved stream."""
+  name = 'metrohast_norm1d'
+  process, args, kwds, keys, g, t = _build(name)
+  spec = oracle.golden_spec(name, g)
+  seed, T = int(g['seeds'][0]), 150
+  rs = np.random.RandomState(seed)
+  w = oracle.stream_width(spec)
+  streams = np.empty((2, T, w, 1))
+  for s in range(T):
+    for c in range(2):   # A's step s, then B's step s
+      streams[c, s, :-1, 0] = rs.random_sample(spec['dim'])
+      streams[c, s, -1, 0] = rs.random_sample()
+  refs = [oracle.run_mh(spec, golden_init(name, 1), streams[c]) for c in range(2)]
+  np.random.seed(seed)
+  a = process.sampler(*args, stop=T, **kwds)
+  b = process.sampler(*args, stop=T, **kwds)
+  got = [[], []]
+  for s in range(T):
+    got[0].append(process.next(a).v[keys[0]])
+    got[1].append(process.next(b).v[keys[0]])
+  for c in range(2):
+    assert _rtol(np.array(got[c]), refs[c]['v_x'][0, :, 0]) <= 1e-12
+  assert a.n_computed <= 3 * T and b.n_computed <= 3 * T, (a.n_computed, b.n_computed)
+  assert np.random.random_sample() == rs.random_sample()
+
+
+def test_samplers_are_not_kept_alive_by_the_registry():
+  """ADVICE r03: SP's counters and last states hold their samplers weakly;
+  after SP.reset() empties the registry, a sampler the caller dropped is
+  collected (and with it its engine's device buffers)."""
+  import gc
+  import weakref
+  process, args, kwds, keys, g, t = _build('metrohast_norm1d')
+  sm = process.sampler(*args, stop=5, **kwds)
+  process._counter[sm] += 3
+  assert process.get_counter(sm) == 3
+  ref = weakref.ref(sm)
+  process.reset()
+  del sm
+  gc.collect()
+  assert ref() is None
+  assert len(process.get_counter()) == 0 and len(process.get_last()) == 0
