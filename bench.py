@@ -151,18 +151,33 @@ def cpu_baseline(budget_s=6.0, chains=65536):
                                            cores, per, budget_s)}
 
 
-def measured_traffic(chains, launch_steps, rng, trace):
+def lib_sha256():
+  """sha256 of the engine library this process loads (probayes_amd._lib)."""
+  import hashlib
+  from probayes_amd import _lib
+  h = hashlib.sha256()
+  with open(_lib.LIB_PATH, 'rb') as f:
+    for blk in iter(lambda: f.read(1 << 20), b''):
+      h.update(blk)
+  return h.hexdigest()
+
+
+def measured_traffic(chains, launch_steps, rng, trace, sha=None):
   """HBM bytes per launch of this exact launch shape (chains, steps in the
-  launch, RNG mode), from the newest profiles/r*_traffic.json (rocprofv3 PMC
-  passes, scripts/profile.sh), or None when no profile matches."""
+  launch, RNG mode) measured on THIS library build: the newest
+  profiles/r*_traffic*.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+  scripts/profile_r04.sh + tools/collect_profiles.py) whose lib_sha256 is the
+  loaded library's; None when no profile of this binary matches."""
   import glob
-  files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic*.json')))
   if not trace:
     return None
+  sha = sha or lib_sha256()
+  files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_traffic*.json')))
   for path in reversed(files):   # newest profile of this kernel and shape
     with open(path) as f:
       t = json.load(f)
-    if (t.get('kernel', '').startswith('mh_pair_kernel') and
+    if (t.get('lib_sha256') == sha and
+        t.get('kernel', '').startswith('mh_pair_kernel') and
         t.get('chains') == chains and t.get('rng', 'philox_fp32') == rng and
         t.get('steps_per_launch') == launch_steps):
       return t['bytes_per_launch']
@@ -281,6 +296,7 @@ def main():
   if rank == 0 and not args.no_cpu_baseline:
     cpu = cpu_baseline()
 
+  sha = lib_sha256()   # the binary the line (and its traffic profile) is of
   from probayes_amd import Engine
   eng = Engine(cfg2_spec(), device=local)
   col = None
@@ -330,7 +346,7 @@ def main():
                      'traffic': args.traffic_bytes if args.traffic_bytes
                                 else measured_traffic(
                                     n, min(spl, args.steps), args.rng,
-                                    not args.no_trace),
+                                    not args.no_trace, sha),
                      'bytes_per_chain_step': bpcs,
                      'kernel': kernel_label(args, n),
                      'avg_launch_ms': avg_launch_s * 1e3,
@@ -340,6 +356,7 @@ def main():
         # of the launches, the HIP-event time of the launches
         'host_enqueue_us': res['enqueue_s'] * 1e6,
         'events_us': kern_ms * 1e3,
+        'lib_sha256': sha,
     }
     if collect_ms is not None:
       line['rccl_allgather_ms'] = collect_ms

@@ -114,6 +114,85 @@ def rewrite(lines, owner, allowed):
   return out, (n, nops, kept), grow
 
 
+# ---------------------------------------------------------------------------
+# Second rewrite: an fp64 accumulate whose accumulator is a fresh copy,
+#     v_mov_b64_e32 vD, vS            (vD = vS)
+#     ...                              (nothing reads or writes vD, writes vS)
+#     v_fmac_f64_e32 vD, A, B          (vD = A B + vD)
+# becomes the one VOP3 instruction v_fma_f64 vD, A, B, vS: the same value in
+# the same register, one VALU instruction fewer (the compiler selects the
+# two-address VOP2 form and copies the accumulator when its old value stays
+# live, e.g. x' = fma(r, scale, x) with x kept for the accept select).  Same
+# bytes (4 + 4 -> 8), so branch offsets keep their range.  Only within a
+# basic block; A must be VOP3-encodable (a VGPR, an SGPR pair -- vS is a
+# VGPR, so one constant-bus read -- or an inline constant; no literal).
+# ---------------------------------------------------------------------------
+REG = re.compile(r'\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]')
+MOV64 = re.compile(r'^(\s*)v_mov_b64_e32\s+v\[(\d+):(\d+)\],\s*v\[(\d+):(\d+)\]\s*(;.*)?$')
+FMAC64 = re.compile(r'^(\s*)v_fmac_f64_e32\s+v\[(\d+):(\d+)\],\s*([^,]+),\s*(v\[\d+:\d+\])\s*(;.*)?$')
+INLINE_F = {'0.5', '-0.5', '1.0', '-1.0', '2.0', '-2.0', '4.0', '-4.0', '0', '1'}
+
+
+def regs(text, kind='v'):
+  """VGPR numbers mentioned in an operand text"""
+  out = set()
+  for m in REG.finditer(text):
+    if m.group(1) == kind:
+      out.add(int(m.group(2)))
+    elif m.group(3) == kind:
+      out.update(range(int(m.group(4)), int(m.group(5)) + 1))
+  return out
+
+
+def ok_a(a):
+  a = a.strip()
+  if re.fullmatch(r'v\[\d+:\d+\]|s\[\d+:\d+\]', a):
+    return True
+  return a in INLINE_F or (INLINE_INT.match(a) is not None and -16 <= int(a) <= 64)
+
+
+def fuse_fmac(lines, allowed, owner):
+  """(rewritten lines, fused count)"""
+  out = list(lines)
+  n = 0
+  pending = {}   # vD lo -> (index of the mov, vD set, vS set, vS text)
+  for i, line in enumerate(lines):
+    body = line.split(';')[0].strip()
+    if LABEL.match(line) or not body or body.startswith('.') or \
+        body.startswith('s_cbranch') or body.startswith('s_branch') or \
+        body.startswith('s_setpc') or body.startswith('s_swappc') or \
+        body.startswith('s_endpgm') or owner[i] not in allowed:
+      pending = {}
+      continue
+    fm = FMAC64.match(line.rstrip('\n'))
+    if fm:
+      d = (int(fm.group(2)), int(fm.group(3)))
+      p = pending.get(d[0])
+      a, b = fm.group(4), fm.group(5)
+      if p is not None and p[1] == set(range(d[0], d[1] + 1)) and ok_a(a) and \
+          not (regs(a) & p[1]) and not (regs(b) & p[1]):
+        out[p[0]] = ''
+        out[i] = '{}v_fma_f64 v[{}:{}], {}, {}, {}\n'.format(
+            fm.group(1), d[0], d[1], a.strip(), b, p[3])
+        n += 1
+        del pending[d[0]]
+        continue
+    mm = MOV64.match(line.rstrip('\n'))
+    # any other instruction: operands it touches end the pending copies
+    # (reads of vD, writes of vD or vS; a conservative textual check: any
+    # mention of the registers)
+    touched = regs(body)
+    for k in [k for k, p in pending.items() if (touched & p[1]) or (touched & p[2])]:
+      del pending[k]
+    if mm:
+      dset = set(range(int(mm.group(2)), int(mm.group(3)) + 1))
+      sset = set(range(int(mm.group(4)), int(mm.group(5)) + 1))
+      if not (dset & sset):
+        pending[int(mm.group(2))] = (i, dset, sset,
+                                     'v[{}:{}]'.format(mm.group(4), mm.group(5)))
+  return [l for l in out if l != ''], n
+
+
 def main():
   src, dst = sys.argv[1], sys.argv[2]
   size = sizes(sys.argv[3] if len(sys.argv) > 3 else None)
@@ -129,8 +208,18 @@ def main():
   _, _, grow = rewrite(lines, owner, set(owner) - {None})
   allowed = {f for f, g in grow.items() if f in size and size[f] + g < LIMIT}
   out, (n, nops, kept), _ = rewrite(lines, owner, allowed)
+  # the fma fusion keeps every function's size (4 + 4 -> 8 bytes): all of them
+  o2 = []
+  func = None
+  for line in out:
+    fm = FUNC.match(line)
+    if fm and not fm.group(1).startswith('.L'):
+      func = fm.group(1)
+    o2.append(func)
+  out, nf = fuse_fmac(out, set(o2) - {None}, o2)
   with open(dst, 'w') as f:
     f.writelines(out)
+  sys.stderr.write('isa_e64: {} mov + fmac_f64 pairs -> v_fma_f64\n'.format(nf))
   big = sorted(set(grow) - allowed)
   sys.stderr.write('isa_e64: {} VOP2 selects -> VOP3 ({} behind an s_nop), {} kept '
                    '({}; {} functions too large to rewrite)\n'.format(

@@ -305,6 +305,9 @@ __device__ __forceinline__ void box_muller_tab(u32x4 w, const BMTables *t,
 __device__ __forceinline__ uint32_t simd_wave_slot() {
   return __builtin_amdgcn_s_getreg(4 | (0 << 6) | (3 << 11));   // HW_ID.WAVE_ID
 }
+__device__ __forceinline__ uint32_t simd_id() {
+  return __builtin_amdgcn_s_getreg(4 | (4 << 6) | (1 << 11));    // HW_ID.SIMD_ID
+}
 __device__ __forceinline__ void fair_prio(uint32_t phase) {
   if (phase & 1u) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
@@ -316,6 +319,8 @@ __device__ __forceinline__ void fair_prio(uint32_t phase) {
 #define PBH_PHASE_DECL uint64_t pbh_tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define PBH_PHASE(k) (pbh_tph[k] = __builtin_amdgcn_s_memrealtime())
 // the loop's quarter points (i of n iterations) into words 5, 6, 7
+// word 4's bits 40..63: a 24-bit tag of the kernel's choosing
+#define PBH_PHASE_TAG(v) (pbh_tph[4] = (uint64_t)(v))
 #define PBH_PHASE_Q(i, n)                                                     \
   do {                                                                        \
     if ((i) == (n) / 4) PBH_PHASE(5);                                         \
@@ -329,13 +334,16 @@ __device__ __forceinline__ void fair_prio(uint32_t phase) {
       uint64_t *pb_ = reinterpret_cast<uint64_t *>(const_cast<double *>(buf)) \
                       + (wave) * 8;                                           \
       for (int k_ = 0; k_ < 8; ++k_) pb_[k_] = pbh_tph[k_];                   \
-      pb_[4] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));          \
+      pb_[4] = (uint64_t)__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)) \
+               | ((uint64_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) << 32) \
+               | ((pbh_tph[4] & 0xFFFFFFull) << 40);                           \
     }                                                                         \
   } while (0)
 #else
 #define PBH_PHASE_DECL
 #define PBH_PHASE(k) ((void)0)
 #define PBH_PHASE_Q(i, n) ((void)0)
+#define PBH_PHASE_TAG(v) ((void)0)
 #define PBH_PHASE_STORE(buf, wave, lane) ((void)0)
 #endif
 
@@ -362,21 +370,36 @@ __device__ __forceinline__ double from_words(uint32_t hi, uint32_t lo) {
 // rolled loop waited for each load in turn, several microseconds of every
 // short launch).  Complete for blocks of >= 256 threads (all kernels here
 // run 256).
-__device__ __forceinline__ void bm64_load(double *lds, const double *g) {
-  constexpr int N2 = kBm64Doubles / 2, T = 256, R = N2 / T;   // 8 full rounds
+// The same in two halves: bm64_issue puts this thread's global loads in
+// flight (registers), bm64_commit writes them to LDS and syncs.  Loads the
+// caller issues in between (the chain state) are waited for only when used:
+// the ds_writes wait for the table's loads alone (vmcnt counts in order).
+struct Bm64Regs {
+  static constexpr int N2 = kBm64Doubles / 2, T = 256, R = N2 / T;   // 8 full rounds
   static_assert(N2 - R * T <= T, "one partial round");
+  double2 v[R], w;
+};
+__device__ __forceinline__ void bm64_issue(const double *g, Bm64Regs &r) {
+  constexpr int N2 = Bm64Regs::N2, T = Bm64Regs::T, R = Bm64Regs::R;
   const int t = (int)(threadIdx.x & (T - 1));   // >= 256 threads: duplicates
   const double2 *src = reinterpret_cast<const double2 *>(g);
+#pragma unroll
+  for (int k = 0; k < R; ++k) r.v[k] = src[t + k * T];
+  r.w = t < N2 - R * T ? src[t + R * T] : double2{0., 0.};
+}
+__device__ __forceinline__ void bm64_commit(double *lds, const Bm64Regs &r) {
+  constexpr int N2 = Bm64Regs::N2, T = Bm64Regs::T, R = Bm64Regs::R;
+  const int t = (int)(threadIdx.x & (T - 1));
   double2 *dst = reinterpret_cast<double2 *>(lds);
-  double2 v[R];
 #pragma unroll
-  for (int k = 0; k < R; ++k) v[k] = src[t + k * T];
-  const bool tail = t < N2 - R * T;
-  double2 w = tail ? src[t + R * T] : double2{0., 0.};
-#pragma unroll
-  for (int k = 0; k < R; ++k) dst[t + k * T] = v[k];
-  if (tail) dst[t + R * T] = w;
+  for (int k = 0; k < R; ++k) dst[t + k * T] = r.v[k];
+  if (t < N2 - R * T) dst[t + R * T] = r.w;
   __syncthreads();
+}
+__device__ __forceinline__ void bm64_load(double *lds, const double *g) {
+  Bm64Regs r;
+  bm64_issue(g, r);
+  bm64_commit(lds, r);
 }
 
 // -2 ln(m 2^e) + offsets for the log table: x = m 2^e (frexp, m in [1/2, 1)),

@@ -81,6 +81,16 @@ struct pbh_engine {
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
   int fair = 11;             // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
   int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
+  // Launches of <= 64 steps (the driver's 20-step shape): the alternation
+  // clock starts at each wave's loop entry and hands over once, half-way
+  // (2^10 ticks = 10.24 us for 20 steps), shifted by fair_off ticks -- the
+  // free-running clock put the one hand-over anywhere in the launch or nowhere
+  // (profiles/r04f_phase.jsonl: the last wave ends 26.4-29.2 us into a k11
+  // launch, 26.5-26.6 us with the launch-relative clock)
+  int fair_short = 10;       // PBH_FAIR_SHORT=k
+  int fair_off = 0;          // PBH_FAIR_OFF=ticks
+  int bal = 0;               // PBH_BAL=D: progress-balanced wave priorities (512 WG)
+  int fair_rel = 0;          // PBH_FAIR_REL=1: long launches use the relative clock too
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
   bool gibbs_mfma = true;    // PBH_GIBBS_MFMA=0 keeps the VALU quadratic form
@@ -198,6 +208,16 @@ int pbh_create(int device, pbh_engine **out) {
   if (device < 0 || device >= nd)
     return fail(PBH_ERR_ARG, "device %d out of range (%d devices)", device, nd);
   HIP_TRY(hipSetDevice(device));
+  // The runtime spins on completion signals instead of yielding / sleeping
+  // on them (hipDeviceScheduleSpin): the host sees a short launch end ~2 us
+  // sooner (tools/ubench/launch_lat.hip, profiles/r04d_launch_lat.jsonl).
+  // Process-wide for the device; a device already in use keeps its flags
+  // (the call then fails, harmlessly).  PBH_SPIN_FLAG=0 leaves the default.
+  {
+    const char *sf = std::getenv("PBH_SPIN_FLAG");
+    if (!sf || sf[0] != '0') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+    (void)hipGetLastError();
+  }
   pbh_engine *e = new pbh_engine();
   e->device = device;
   if (const char *np = std::getenv("PBH_NO_PAIR")) e->pair_enabled = np[0] != '1';
@@ -216,6 +236,11 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::min(20, std::max(0, std::atoi(fa)));
   if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
+  if (const char *fs = std::getenv("PBH_FAIR_SHORT"))
+    e->fair_short = std::min(20, std::max(0, std::atoi(fs)));
+  if (const char *b = std::getenv("PBH_BAL")) e->bal = std::min(64, std::max(0, std::atoi(b)));
+  if (const char *fr = std::getenv("PBH_FAIR_REL")) e->fair_rel = std::atoi(fr) != 0;
+  if (const char *fo = std::getenv("PBH_FAIR_OFF")) e->fair_off = std::atoi(fo);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
@@ -962,7 +987,8 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
   k.fair = e->fair;
-  k.pair_wg = e->pair_wg;
+  k.pair_wg = e->bal ? 512 : e->pair_wg;
+  k.bal = e->bal;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;
@@ -988,6 +1014,10 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     const int64_t m = std::min(spl, n_steps - done);
     if (!e->event_markers && done + m >= n_steps) lev.stop = e->ev1;
     k.n_steps = (int32_t)m;
+    const bool short_launch = m <= 64;
+    k.fair = short_launch ? e->fair_short : e->fair;
+    k.fair_rel = short_launch ? 1 : e->fair_rel;
+    k.fair_off = short_launch ? e->fair_off : 0;
     k.g0 = e->g;
     k.has_pred = e->has_pred ? 1 : 0;
     k.rep_row0 = e->g - e->rep_g0;

@@ -1135,6 +1135,12 @@ void mh_pair_kernel(KArgs a) {
   const uint32_t bstride = (uint32_t)(a.n * 8);
   const uint32_t loff = (uint32_t)(cc * 8);
 
+  // FULL: the LDS table's loads go first, so that the first pair's draws
+  // (which need only the table) wait for them alone and run while the chain
+  // state's loads below are still in flight
+  Bm64Regs tabr;
+  if constexpr (FULL) bm64_issue(a.bm64, tabr);
+
   // Per-lane model constants in VGPRs for the whole launch (the half's dims
   // differ between lanes, so these are vector values, loaded once).
   double psc[H], plc[H], ca[H], cb[H], cc2[H];
@@ -1169,8 +1175,17 @@ void mh_pair_kernel(KArgs a) {
   Xo xs{0u, 0u, 0u, 0u};
   if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, h, cc);
 
+  // FULL with a.bal: the SIMD's two waves (one 512-thread workgroup) post
+  // their progress in LDS; the slot counters are zeroed before the table
+  // load's barrier
+  __shared__ uint32_t s_prog[8], s_cnt[4];
+  if (FULL && threadIdx.x < 8) {
+    s_prog[threadIdx.x] = 0u;
+    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0u;
+  }
   // the LDS tables after the state's loads: all of them in flight at once
-  if constexpr (TAB) bm64_load(s_bmt, a.bm64);
+  if constexpr (FULL) bm64_commit(s_bmt, tabr);
+  else if constexpr (TAB) bm64_load(s_bmt, a.bm64);
 
   // record phase / index of the trace, advanced per step (no 64-bit
   // division in the loop): step g records iff (g + 1) % thin == 0, at
@@ -1178,8 +1193,9 @@ void mh_pair_kernel(KArgs a) {
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
   // Drain the entry loads here: a wait for them inside the loop would also
-  // wait for every trace store issued before it.
-  __builtin_amdgcn_s_waitcnt(0);
+  // wait for every trace store issued before it.  (FULL drains after the
+  // first pair's draws, before its first step.)
+  if constexpr (!FULL) __builtin_amdgcn_s_waitcnt(0);
   PBH_PHASE(1);
 
   // One chain-step.  (r, t0, t1) are this step's draws (Philox: supplied by
@@ -1373,6 +1389,19 @@ void mh_pair_kernel(KArgs a) {
         const uint32_t abytes = (uint32_t)(a.W * 8);
         int64_t rec = a.g0 + s - a.rec_base;   // thin 1: record = step
         const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);
+        // blocks Q0 .. NB-1 of pair P (the words before block Q0 unused)
+        auto philox_from = [&](int64_t P, uint32_t (&w)[4 * NB], auto Q0) {
+#pragma unroll
+          for (int q = 0; q < 4 * decltype(Q0)::value; ++q) w[q] = 0u;
+#pragma unroll
+          for (int q = decltype(Q0)::value; q < NB; ++q) {
+            const u32x4 b = philox4x32_10_rk(ctr(q + 16 * h, P, chain), rk);
+            w[4 * q] = b.x;
+            w[4 * q + 1] = b.y;
+            w[4 * q + 2] = b.z;
+            w[4 * q + 3] = b.w;
+          }
+        };
         auto philox = [&](int64_t P, uint32_t (&w)[4 * NB]) {
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
@@ -1453,9 +1482,13 @@ void mh_pair_kernel(KArgs a) {
         using IA = std::integral_constant<int, QA>;
         using IH = std::integral_constant<int, H>;
         if (a.g0 & 1) {   // launch starts on a pair's 2nd step
+          // only step B's normals: Box-Muller pairs H/2 .. H-1 and the lead
+          // word, i.e. the blocks from the one holding word 3 (H / 2) on
+          constexpr int QB = 3 * (H / 2) / 4;
           uint32_t w[4 * NB];
-          philox(a.g0 >> 1, w);
+          philox_from(a.g0 >> 1, w, std::integral_constant<int, QB>{});
           normals(w, std::integral_constant<int, H / 2>{}, IH{}, cA, cB);
+          __builtin_amdgcn_s_waitcnt(0);   // the entry loads, before the first step
           step_full(0, cB, w[3 * H] & 0xFFFFu);
           s = 1;
         }
@@ -1465,10 +1498,47 @@ void mh_pair_kernel(KArgs a) {
           normals(w, I0{}, IH{}, cA, cB);
           ctA = w[3 * H] >> 16;
           ctB = w[3 * H] & 0xFFFFu;
+          if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // no stores in flight yet
           PBH_PHASE(2);
           const uint32_t slot = a.fair ? simd_wave_slot() : 0u;
+          // a.bal: this wave's and its SIMD partner's progress slots
+          uint32_t me = 0u, partner = 0u;
+          if (a.bal) {
+            const uint32_t simd = simd_id();
+            uint32_t idx = 0u;
+            if (lane == 0) idx = __hip_atomic_fetch_add(&s_cnt[simd], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            idx = __builtin_amdgcn_readfirstlane(idx) & 1u;
+            me = 2u * simd + idx;
+            partner = me ^ 1u;
+            PBH_PHASE_TAG(me + 1u);
+          }
+          uint32_t other = 0u;   // the partner's progress read one pair ago
+          // a.fair_rel: the alternation's clock starts at this wave's loop
+          // entry (the waves of a launch start within ~0.4 us of each other),
+          // so the hand-overs of a short launch fall at the same points of
+          // every launch instead of wherever the free-running clock is
+          const uint64_t tfair0 =
+              a.fair_rel ? __builtin_amdgcn_s_memrealtime() + (int64_t)a.fair_off : 0ull;
           for (; s + 3 < a.n_steps; s += 2) {
-            if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
+            if (a.bal) {
+              // the wave that is more than a.bal pairs behind its partner
+              // takes the lead (priority 1) until it is a.bal pairs ahead:
+              // a leader / filler interleave whose roles trade, so both waves
+              // end together instead of the younger one finishing alone
+              const int mine = s >> 1;
+              const int gap = (int)__builtin_amdgcn_readfirstlane(other) - mine;
+              if (gap > a.bal) __builtin_amdgcn_s_setprio(1);
+              else if (gap < -a.bal) __builtin_amdgcn_s_setprio(0);
+              if (lane == 0)
+                __hip_atomic_store(&s_prog[me], (uint32_t)mine, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+              other = __hip_atomic_load(&s_prog[partner], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (a.fair) {
+              const int64_t el = (int64_t)(__builtin_amdgcn_s_memrealtime() - tfair0);
+              fair_prio((uint32_t)((el > 0 ? (uint64_t)el : 0ull) >> a.fair) + slot);
+            }
             PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
             uint32_t nw[4 * NB];
             double nA[H], nB[H];
@@ -1493,6 +1563,7 @@ void mh_pair_kernel(KArgs a) {
           uint32_t w[4 * NB];
           philox((a.g0 + s) >> 1, w);
           normals(w, I0{}, IA{}, cA, cB);
+          if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // a one-step launch
           step_full(s, cA, w[3 * H] >> 16);
         }
         PBH_PHASE(3);
@@ -1890,6 +1961,15 @@ __device__ __forceinline__ float qperm_f32(float v) {
                                        __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
 
+// the same permutation for a summand: old = 0.0f and bound_ctrl set, the
+// form GCNDPPCombine folds into the consuming v_add_f32 (quad_perm reads a
+// valid lane everywhere, so the result is qperm_f32's)
+template <int CTRL>
+__device__ __forceinline__ float qperm_add_f32(float v) {
+  return __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_update_dpp(
+                                       0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
 // The rare undecided step of the quad kernel (accept_filter_ms32's need):
 // the exact ratio form of (lp', lp) on t's full 53 bits, out of line so that
 // the steady-state loop keeps neither its registers nor its code.
@@ -2052,8 +2132,10 @@ void mh_gmm_quad_kernel(KArgs a) {
       // exp(-inf) = 0 in both paths without a select (exp_tab clamps at -746:
       // 0 to within 2^-1074)
       float e32 = __builtin_amdgcn_exp2f((float)((v - lm) * 1.4426950408889634));
-      e32 = e32 + qperm_f32<kQuadXor1>(e32);
-      const float E32 = e32 + qperm_f32<kQuadXor2>(e32);   // the proposal's sum
+      // (update_dpp with old = 0 and bound_ctrl: the DPP combiner folds
+      // each move into the add, v_add_f32_dpp, one VALU per round)
+      e32 = e32 + qperm_add_f32<kQuadXor1>(e32);
+      const float E32 = e32 + qperm_add_f32<kQuadXor2>(e32);   // the proposal's sum
       // record path (off the decision's chain): M' and S in fp64
       // v_max_f64 without the compiler's canonicalising max of the DPP'd
       // operand (the values are never NaN: finite or -inf)

@@ -65,8 +65,21 @@ for m in lens:
       raise SystemExit('missing stamps: {} waves'.format(int((st == 0).any(1).sum())))
     t0 = st[:, 0].min()
     us = (st - t0) * 0.01   # 100 MHz ticks -> us
-    slot = w8[:, 4] & 0xF   # HW_ID.WAVE_ID: the wave's slot on its SIMD
-    row = {'tag': tag, 'steps': m, 'rep': rep, 'events_us': ms * 1e3}
+    # the wave's slot on its SIMD: HW_ID.WAVE_ID [3:0]; the SIMD itself is
+    # HW_ID [15:4] (simd, pipe, cu, sh, se) + XCC_ID (word 4 bits 32..35)
+    w4 = buf.reshape(waves, 8)[:, 4].astype(np.uint64)
+    hw = (((w4 >> np.uint64(4)) & np.uint64(0xFFF)) |
+          (((w4 >> np.uint64(32)) & np.uint64(0xF)) << np.uint64(12))).astype(np.int64)
+    slot = (w4 & np.uint64(0xF)).astype(np.int64)
+    order = np.lexsort((slot, hw))
+    same = np.concatenate([[False], hw[order][1:] == hw[order][:-1]])
+    # the waves of one SIMD in one workgroup? (wave index // waves per WG)
+    wpg = int(os.environ.get('PHASE_WPG', '4'))
+    grp = np.arange(len(hw)) // wpg
+    pair_same_wg = float(np.mean(grp[order][1:][same[1:]] == grp[order][:-1][same[1:]])) \
+        if same.any() else float('nan')
+    row = {'tag': tag, 'steps': m, 'rep': rep, 'events_us': ms * 1e3,
+           'simd_pairs_same_wg': pair_same_wg}
     for k, name in enumerate(['entry', 'loaded', 'drawn', 'q1', 'q2', 'q3', 'loop_end']):
       row[name] = [round(float(np.percentile(us[:, k], q)), 2) for q in (0, 50, 100)]
       row[name + '_slots'] = [round(float(np.median(us[slot == v, k])), 2) for v in (0, 1)]
