@@ -1992,7 +1992,11 @@ __device__ __attribute__((noinline)) bool gmm_quad_exact(
 // the plain ratio form (acc_beta = 1) -- no per-step range, record or
 // first-step tests, and branch-free stores: a lane with nothing of its own
 // to write (a part p >= D, or a padding chain, which runs chain 0's exact
-// trajectory) rewrites the identical value of a lane that has.
+// trajectory) rewrites the identical value of a lane that has.  Its steps
+// run only the fp32 decision path; the fp64 record path (the state's M and
+// S, i.e. v.prob) is evaluated once per group per lane (round 4: ~100 -> ~65
+// VALU per wave-step), bit-identical to the general form's per-step records
+// (test_gmm_quad_steady_state_form_is_the_general_form).
 // LOC0: every proposal loc is 0 (the examples' norm.rvs(scale=...)): x' =
 // fma(r, scale, x), one rounding, instead of x + fma(r, scale, loc).
 template <int D, int K, bool MOM, bool FULL, bool LOC0 = false>
@@ -2043,7 +2047,6 @@ void mh_gmm_quad_kernel(KArgs a) {
   PBH_PHASE(1);
 
   const int64_t gend = a.g0 + a.n_steps;
-  uint64_t inlm = __ballot(__builtin_fabs(lm) <= 698.);   // FULL: |lm| <= 698
   // FULL: lane p < D writes dim p's record row, the others nothing (the
   // buffer range check: no select of the dim, no branch)
   uint32_t xoffm[D];
@@ -2059,63 +2062,203 @@ void mh_gmm_quad_kernel(KArgs a) {
   if constexpr (FULL) lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
   PBH_PHASE(2);
   const uint32_t slot = FULL && a.fair ? simd_wave_slot() : 0u;
-  for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
-    if (FULL && a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
-    if constexpr (FULL) PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
-    // ---- lane p draws step 4 G + p; the quad shares the group's draws
-    double rown[D];
-    uint32_t lown;
-    if constexpr (FULL) {
+  if constexpr (FULL) {
+    // ---- steady state with the record path deferred to the group's end ----
+    // Per step only the decision path runs: this lane's component term of the
+    // proposal, its fp32 weight relative to the group's reference R (the
+    // state's max at the group start) and the quad's fp32 sum E32, against
+    // the state's sum ls32 (relative to the same R; on accept ls32 = E32).
+    // The recorded v.prob of step 4 G + p is lane p's after the group: the
+    // state after that step (its x staged in LDS) re-evaluated -- every
+    // component's term, M = max, S = (e0 + e1) + (e2 + e3), M + ln S: the same
+    // operations on the same values as the general form's per-step (M, S),
+    // so the same bits -- or lp0 while no step of this launch has accepted.
+    // Decisions are the fp64 ratio form's (filter with a 8e-6 margin, the
+    // exact form for the rest): |y| <= 40 (log2) on every fp32 weight used.
+    __shared__ double s_xs[4 * D * kBlock];   // the state after each step
+    double kcw[4], kc0[4], kcmw[4][D];          // every component (uniform)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = k < K;
+      kcw[k] = ok ? cld(a.tw, k) : 0.;
+      kc0[k] = ok ? cld(a.tw, K + k) : -__builtin_inf();
+#pragma unroll
+      for (int i = 0; i < D; ++i) kcmw[k][i] = ok ? cld(a.tb, k * D + i) * kcw[k] : 0.;
+    }
+    const double e_absent = exp_tab(-__builtin_inf(), s_bmt);   // exp of a -inf term
+    constexpr float kLw = 1.0f / (float)(1u << LB);
+    constexpr uint64_t kQ0 = 0x1111111111111111ull;
+    double R = lp0;          // the decision's reference (group start)
+    uint64_t initm = ~0ull;  // lanes whose chain has not accepted in this launch
+    uint64_t rinm = __ballot(__builtin_fabs(R) <= 650.);
+    uint64_t sinm = ~0ull;   // ls32 within [2^-40, 2^40]
+    const uint64_t allm = __ballot(true);
+    for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
+      if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
+      PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
+      double rown[D];
 #pragma unroll
       for (int i = 0; i < D; ++i) rown[i] = rnext[i];
-      lown = lnext;
-    } else {
-      lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
+      const uint32_t lown = lnext;
+      const float tlown = (float)lown * kLw;
+      uint32_t wn[4 * NB];   // group G + 1's words
+      auto next_blocks = [&]() {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const u32x4 b = philox4x32_10(ctr(q, 4 * (G + 1) + p, chain), a.seed_lo, a.seed_hi);
+          wn[4 * q] = b.x;
+          wn[4 * q + 1] = b.y;
+          wn[4 * q + 2] = b.z;
+          wn[4 * q + 3] = b.w;
+        }
+      };
+      auto next_normals = [&]() {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          double z0, z1;
+          bm96_pair(wn[3 * q], wn[3 * q + 1], wn[3 * q + 2], s_bmt, z0, z1);
+          rnext[2 * q] = z0;
+          if (2 * q + 1 < D) rnext[2 * q + 1] = z1;
+        }
+        lnext = wn[3 * NP] >> (32 - kStepLead);
+      };
+      double *const gtx = wave_uniform(txrow);
+      uint16_t *const gacc = wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W));
+      uint64_t ginit[4];
+      // the quad's (M, S) of a term v (the general form's record arithmetic)
+      auto quad_ms = [&](double v, double &M, double &S) {
+        M = max_f64_raw(v, qperm_f64<kQuadXor1>(v));
+        M = max_f64_raw(M, qperm_f64<kQuadXor2>(M));
+        double e = exp_tab(v - M, s_bmt);
+        e = e + qperm_f64<kQuadXor1>(e);
+        S = e + qperm_f64<kQuadXor2>(e);
+      };
+      auto term = [&](const double (&xv)[D], double cwv, double c0v, const double (&cm)[D]) {
+        double v = c0v;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          const double u = __builtin_fma(xv[i], cwv, -cm[i]);
+          v = __builtin_fma(-u, u, v);
+        }
+        return v;
+      };
+      auto step = [&](auto J) {
+        constexpr int j = decltype(J)::value;
+        double r[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
+        const int64_t g = 4 * G + j;
+        double xp[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+          xp[i] = LOC0 ? __builtin_fma(r[i], psc[i], x[i]) : x[i] + __builtin_fma(r[i], psc[i], plc[i]);
+        const double v = term(xp, cw, c0, cmw);
+        float e32 = __builtin_amdgcn_exp2f((float)((v - R) * 1.4426950408889634));
+        e32 = e32 + qperm_add_f32<kQuadXor1>(e32);
+        const float E32 = e32 + qperm_add_f32<kQuadXor2>(e32);
+        const float tlo = qperm_f32<j * 85>(tlown);
+        const float thi = tlo + kLw;
+        const uint64_t pinm = __ballot((E32 >= 0x1p-40f) & (E32 <= 0x1p40f));
+        const uint64_t inrm = rinm & sinm & pinm;
+        const uint64_t af = __ballot(thi * ls32 <= E32 * 0.999992f);
+        const uint64_t rf = __ballot(tlo * ls32 > E32 * 1.000008f);
+        uint64_t accm = inrm & af;
+        const uint64_t needm = ~(inrm & (af | rf)) & allm;
+        if (needm) {   // wave-uniform, rare: the exact ratio form in fp64
+          double M, S, ms_, ss_;
+          quad_ms(v, M, S);                            // the proposal
+          quad_ms(term(x, cw, c0, cmw), ms_, ss_);     // the state
+          const bool st0 = __builtin_amdgcn_inverse_ballot_w64(initm);
+          const double lm_ = st0 ? lp0 : ms_, ls_ = st0 ? 1.0 : ss_;
+          const uint32_t ld = qperm_u32<j * 85>(lown);
+          bool ex = false;
+          if (__builtin_amdgcn_inverse_ballot_w64(needm))
+            ex = gmm_quad_exact(a.seed_lo, a.seed_hi, a.acc_beta, a.log_npi, s_bmt,
+                                g, chain, ld, M, S, lm_, ls_, lp0);
+          accm = (accm & ~needm) | (__ballot(ex) & needm);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) x[i] = sel_f64(accm, x[i], xp[i]);
+        ls32 = __builtin_amdgcn_inverse_ballot_w64(accm) ? E32 : ls32;
+        sinm = (sinm & ~accm) | (pinm & accm);
+        initm &= ~accm;
+        ginit[j] = initm;
+        if constexpr (MOM) {
+          nacc += __builtin_amdgcn_inverse_ballot_w64(accm) ? 1 : 0;
+          double xo = x[0];
+#pragma unroll
+          for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
+          ms += xo;
+          mq = __builtin_fma(xo, xo, mq);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          st_buf_n(gtx + j * rstride, rbytes, xoffm[i], x[i]);
+          s_xs[(j * D + i) * kBlock + threadIdx.x] = x[i];
+        }
+        uint64_t m = accm & kQ0 & act_bits;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0xFFFFull;
+        // every lane stores the wave's word (one address, one value)
+        st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), (uint16_t)m);
+      };
+      next_blocks();
+      step(std::integral_constant<int, 0>{});
+      next_normals();
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+      // ---- the group's records: lane p, the state after step 4 G + p ----
+      double xs[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) xs[i] = s_xs[(p * D + i) * kBlock + threadIdx.x];
+      const uint64_t pinit = (ginit[0] & kQ0) | (ginit[1] & (kQ0 << 1)) |
+                             (ginit[2] & (kQ0 << 2)) | (ginit[3] & (kQ0 << 3));
+      double vk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) vk[k] = k < K ? term(xs, kcw[k], kc0[k], kcmw[k]) : -__builtin_inf();
+      const double M = max_f64_raw(max_f64_raw(vk[0], vk[1]), max_f64_raw(vk[2], vk[3]));
+      double ek[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ek[k] = k < K ? exp_tab(vk[k] - M, s_bmt) : e_absent;
+      const double S = (ek[0] + ek[1]) + (ek[2] + ek[3]);
+      const bool pi0 = __builtin_amdgcn_inverse_ballot_w64(pinit);
+      const double pm = pi0 ? lp0 : M, pss = pi0 ? 1.0 : S;
+      const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
+      st_buf(wave_uniform(a.tlp + ri * a.n), lpoff, 0, lpr);
+      // the next group's reference: the state after step 4 G + 3 (lane 3)
+      R = qbcast_f64<3>(pm);
+      lm = R;
+      ls = qbcast_f64<3>(pss);
+      ls32 = (float)ls;
+      rinm = __ballot(__builtin_fabs(R) <= 650.);
+      sinm = allm;   // ls in [1, K] (or 1)
+      ri += 4;
+      txrow += 4 * rstride;
     }
-    uint32_t wn[4 * NB];   // FULL: group G + 1's words
-    auto next_blocks = [&]() {
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const u32x4 b = philox4x32_10(ctr(q, 4 * (G + 1) + p, chain), a.seed_lo, a.seed_hi);
-        wn[4 * q] = b.x;
-        wn[4 * q + 1] = b.y;
-        wn[4 * q + 2] = b.z;
-        wn[4 * q + 3] = b.w;
-      }
-    };
-    auto next_normals = [&]() {
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        double z0, z1;
-        bm96_pair(wn[3 * q], wn[3 * q + 1], wn[3 * q + 2], s_bmt, z0, z1);
-        rnext[2 * q] = z0;
-        if (2 * q + 1 < D) rnext[2 * q + 1] = z1;
-      }
-      lnext = wn[3 * NP] >> (32 - kStepLead);
-    };
-    // FULL: the threshold lead as the float the filter compares (the same
-    // value accept_filter_rel32 forms), converted once per group and lane
-    constexpr float kLw = 1.0f / (float)(1u << LB);
-    const float tlown = FULL ? (float)lown * kLw : 0.f;
+  } else {
+  // ---- the general form: any launch (partial groups, thinning, step 1,
+  // tempered ratio forms), the state carried as (M, S) step by step
+  for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
+    // ---- lane p draws step 4 G + p; the quad shares the group's draws
+    double rown[D];
+    const uint32_t lown = step_draws<D>(a, 4 * G + p, chain, s_bmt, rown);
     double gm[4], gs[4];     // the group's states (M, S), for the records
     int64_t grec[4];
-    // FULL: the group's record rows as scalar buffer bases, one pair of
-    // readfirstlanes per group (step j stores at byte offset j * row bytes)
-    double *const gtx = FULL ? wave_uniform(txrow) : nullptr;
-    uint16_t *const gacc = FULL ? wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W))
-                                : nullptr;
     // one step of the group; j is a compile-time constant (DPP controls)
     auto step = [&](auto J) {
       constexpr int j = decltype(J)::value;
       double r[D];
 #pragma unroll
       for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
-      const uint32_t lead = FULL ? 0u : qperm_u32<j * 85>(lown);
+      const uint32_t lead = qperm_u32<j * 85>(lown);
       const int64_t g = 4 * G + j;
       grec[j] = -1;
       gm[j] = lm;
       gs[j] = ls;
-      if (!FULL && (g < a.g0 || g >= gend)) return;   // wave-uniform
+      if (g < a.g0 || g >= gend) return;   // wave-uniform
       const int s = (int)(g - a.g0);
       double xp[D];
 #pragma unroll
@@ -2147,29 +2290,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       e = e + qperm_f64<kQuadXor1>(e);
       const double S = e + qperm_f64<kQuadXor2>(e);   // in [1, K]
       bool acc;
-      uint64_t accm = 0;   // FULL: the decisions as a lane mask
-      if constexpr (FULL) {
-        // the state's range bit is carried as a mask (inlm) through the
-        // selects; accept_filter_rel32_mask on the broadcast float lead
-        const uint64_t inMm = __ballot(__builtin_fabs(M) <= 698.);
-        const uint64_t inrm = inMm & inlm;
-        const float tlo = qperm_f32<j * 85>(tlown);
-        const float thi = tlo + kLw;
-        const uint64_t af = __ballot(thi * ls32 <= E32 * 0.999996f);
-        const uint64_t rf = __ballot(tlo * ls32 > E32 * 1.000004f);
-        accm = inrm & af;
-        const uint64_t needm = ~(inrm & (af | rf)) & __ballot(true);
-        if (needm) {   // wave-uniform, rare
-          const uint32_t ld = qperm_u32<j * 85>(lown);
-          bool ex = false;
-          if (__builtin_amdgcn_inverse_ballot_w64(needm))
-            ex = gmm_quad_exact(a.seed_lo, a.seed_hi, a.acc_beta, a.log_npi, s_bmt,
-                                g, chain, ld, M, S, lm, ls, lp0);
-          accm = (accm & ~needm) | (__ballot(ex) & needm);
-        }
-        inlm = (inlm & ~accm) | (inMm & accm);
-        acc = __builtin_amdgcn_inverse_ballot_w64(accm);
-      } else if (!a.has_pred && s == 0) {
+      if (!a.has_pred && s == 0) {
         acc = true;                                  // s = None on step 1
       } else {
         const Decision dc = a.acc_beta == 1.0
@@ -2188,19 +2309,11 @@ void mh_gmm_quad_kernel(KArgs a) {
           }
         }
       }
-      if constexpr (FULL) {   // selects on the mask (no bool round trip)
-#pragma unroll
-        for (int i = 0; i < D; ++i) x[i] = sel_f64(accm, x[i], xp[i]);
-        lm = sel_f64(accm, lm, M);
-        ls = sel_f64(accm, ls, S);
-        ls32 = (float)ls;   // fp32 of the selected S (no select of its own)
-      } else {
 #pragma unroll
         for (int i = 0; i < D; ++i) x[i] = acc ? xp[i] : x[i];
         lm = acc ? M : lm;
         ls = acc ? S : ls;
         ls32 = (float)ls;
-      }
       gm[j] = lm;
       gs[j] = ls;
       if constexpr (MOM) {
@@ -2210,23 +2323,6 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int i = 1; i < D; ++i) xo = p == i ? x[i] : xo;
         ms += xo;
         mq = __builtin_fma(xo, xo, mq);
-      }
-      if constexpr (FULL) {
-        // the record row is wave-uniform: a scalar buffer resource (without
-        // readfirstlane the compiler wraps the store in a waterfall loop)
-#pragma unroll
-        for (int i = 0; i < D; ++i) st_buf_n(gtx + j * rstride, rbytes, xoffm[i], x[i]);
-        grec[j] = ri;
-        uint64_t m = accm & 0x1111111111111111ull & act_bits;
-        m = (m | (m >> 3)) & 0x0303030303030303ull;
-        m = (m | (m >> 6)) & 0x000F000F000F000Full;
-        m = (m | (m >> 12)) & 0x000000FF000000FFull;
-        m = (m | (m >> 24)) & 0xFFFFull;
-        // every lane stores the wave's word (one address, one value)
-        st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), (uint16_t)m);
-        ++ri;
-        txrow += rstride;
-        return;
       }
       const bool rec_now = ph == 0;
       const int64_t rec = ri;
@@ -2255,9 +2351,7 @@ void mh_gmm_quad_kernel(KArgs a) {
           reinterpret_cast<uint16_t *>(a.tacc)[rec * 4 * a.W + wave] = (uint16_t)m;
       }
     };
-    if constexpr (FULL) next_blocks();
     step(std::integral_constant<int, 0>{});
-    if constexpr (FULL) next_normals();
     step(std::integral_constant<int, 1>{});
     step(std::integral_constant<int, 2>{});
     step(std::integral_constant<int, 3>{});
@@ -2270,14 +2364,11 @@ void mh_gmm_quad_kernel(KArgs a) {
       pss = p == j ? gs[j] : pss;
       prec = p == j ? grec[j] : prec;
     }
-    if constexpr (FULL) {
-      // records ri - 4 .. ri - 1 (lane p: step 4 G + p): a uniform base
-      const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
-      st_buf(wave_uniform(a.tlp + (ri - 4) * a.n), lpoff, 0, lpr);
-    } else if (prec >= 0 && active) {
+    if (prec >= 0 && active) {
       const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
       __builtin_nontemporal_store(lpr, &a.tlp[prec * a.n + cc]);
     }
+  }
   }
   PBH_PHASE(3);
   if (active) {
