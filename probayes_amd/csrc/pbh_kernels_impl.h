@@ -2093,6 +2093,11 @@ void mh_gmm_quad_kernel(KArgs a) {
     uint64_t rinm = __ballot(__builtin_fabs(R) <= 650.);
     uint64_t sinm = ~0ull;   // ls32 within [2^-40, 2^40]
     const uint64_t allm = __ballot(true);
+    // accept words: lane c < 16 reads lane 4 c (chain c of the wave); act16 =
+    // the wave's active chains as the word's bits
+    const int bperm4 = (lane & 15) * 16;
+    const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);   // SGPRs stay free
+    const uint64_t act16 = __ballot(lane < 16 && wave * 16 + lane < a.n);
     for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
       if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
       PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
@@ -2105,7 +2110,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       auto next_blocks = [&]() {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const u32x4 b = philox4x32_10(ctr(q, 4 * (G + 1) + p, chain), a.seed_lo, a.seed_hi);
+          const u32x4 b = philox4x32_10_rk(ctr(q, 4 * (G + 1) + p, chain), rk);
           wn[4 * q] = b.x;
           wn[4 * q + 1] = b.y;
           wn[4 * q + 2] = b.z;
@@ -2124,7 +2129,7 @@ void mh_gmm_quad_kernel(KArgs a) {
       };
       double *const gtx = wave_uniform(txrow);
       uint16_t *const gacc = wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W));
-      uint64_t ginit[4];
+      uint64_t ginit[4], gacm[4];
       // the quad's (M, S) of a term v (the general form's record arithmetic)
       auto quad_ms = [&](double v, double &M, double &S) {
         M = max_f64_raw(v, qperm_f64<kQuadXor1>(v));
@@ -2196,13 +2201,7 @@ void mh_gmm_quad_kernel(KArgs a) {
           st_buf_n(gtx + j * rstride, rbytes, xoffm[i], x[i]);
           s_xs[(j * D + i) * kBlock + threadIdx.x] = x[i];
         }
-        uint64_t m = accm & kQ0 & act_bits;
-        m = (m | (m >> 3)) & 0x0303030303030303ull;
-        m = (m | (m >> 6)) & 0x000F000F000F000Full;
-        m = (m | (m >> 12)) & 0x000000FF000000FFull;
-        m = (m | (m >> 24)) & 0xFFFFull;
-        // every lane stores the wave's word (one address, one value)
-        st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), (uint16_t)m);
+        gacm[j] = accm;
       };
       next_blocks();
       step(std::integral_constant<int, 0>{});
@@ -2210,6 +2209,23 @@ void mh_gmm_quad_kernel(KArgs a) {
       step(std::integral_constant<int, 1>{});
       step(std::integral_constant<int, 2>{});
       step(std::integral_constant<int, 3>{});
+      {
+        // the group's accept words: lane c < 16 takes chain c's four decision
+        // bits from its quad (lane 4 c, ds_bpermute) and each step's word is
+        // one ballot -- instead of compressing every step's 64-bit mask on
+        // the SALU
+        uint32_t vf = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          vf |= __builtin_amdgcn_inverse_ballot_w64(gacm[j]) ? (1u << j) : 0u;
+        const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute(bperm4, (int)vf);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint16_t w16 = (uint16_t)(__ballot((fl >> j) & 1u) & act16);
+          // every lane stores the wave's word (one address, one value)
+          st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), w16);
+        }
+      }
       // ---- the group's records: lane p, the state after step 4 G + p ----
       double xs[D];
 #pragma unroll
