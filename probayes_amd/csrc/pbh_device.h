@@ -541,6 +541,18 @@ __device__ __forceinline__ void st_buf_n(double *base, uint32_t nbytes,
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
                                         (int)voff, 0, 2);
 }
+// The same with a wave-uniform byte offset soff: the range check covers
+// voff + soff (measured on gfx950, tools/ubench/soffset_range.hip), so a
+// loop-invariant resource over a launch's whole span of rows takes the row
+// as soff (one scalar add per step instead of a new resource per store).
+__device__ __forceinline__ void st_buf_ns(double *base, uint32_t nbytes, uint32_t voff,
+                                          uint32_t soff, double v) {
+  typedef unsigned int u32x2_t __attribute__((__vector_size__(8)));
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs,
+                                        (int)voff, (int)soff, 2);
+}
 __device__ __forceinline__ void st_buf32_n(uint32_t *base, uint32_t nbytes,
                                            uint32_t voff, uint32_t v) {
   const __amdgpu_buffer_rsrc_t rs =
@@ -569,6 +581,26 @@ __device__ __forceinline__ double sel_f64(uint64_t m, double if0, double if1) {
 __device__ __forceinline__ float sel_f32(uint64_t m, float if0, float if1) {
   return __builtin_bit_cast(float, sel_u32(m, __builtin_bit_cast(uint32_t, if0),
                                            __builtin_bit_cast(uint32_t, if1)));
+}
+
+// A uniform prior's limits as closed ones: for every double x, x > lo is
+// x >= lo_closed(lo, false) and x >= lo is x >= lo_closed(lo, true) (a NaN
+// limit compares false both ways); likewise x < hi is x <= hi_closed(hi,
+// false).  One compare per limit and dim in the steady-state kernels instead
+// of a compare, an equality test and a wave-uniform branch on the flag.
+__device__ __forceinline__ double lo_closed(double lo, bool incl) {
+  if (incl || lo != lo) return lo;
+  if (lo == __builtin_inf()) return __builtin_nan("");   // x > +inf: never
+  if (lo == 0.) return 0x1p-1074;                        // x > 0: x >= the least denormal
+  const int64_t b = __builtin_bit_cast(int64_t, lo);
+  return __builtin_bit_cast(double, lo > 0. ? b + 1 : b - 1);   // the next double up
+}
+__device__ __forceinline__ double hi_closed(double hi, bool incl) {
+  if (incl || hi != hi) return hi;
+  if (hi == -__builtin_inf()) return __builtin_nan("");
+  if (hi == 0.) return -0x1p-1074;
+  const int64_t b = __builtin_bit_cast(int64_t, hi);
+  return __builtin_bit_cast(double, hi > 0. ? b - 1 : b + 1);   // the next double down
 }
 
 // 1/x and 1/sqrt(x) for positive normal x: the hardware v_rcp_f64 /

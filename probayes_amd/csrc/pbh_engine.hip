@@ -79,6 +79,7 @@ struct pbh_engine {
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
   bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
+  bool iid_pair = false;     // PBH_IID_PAIR=1: the steady-state iid kernel on lane pairs (measured slower)
   int fair = 11;             // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
   int pair_wg = 256;         // PBH_PAIR_WG=512: FULL pair kernel in 8-wave workgroups
   // Launches of <= 64 steps (the driver's 20-step shape): the alternation
@@ -234,6 +235,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
+  if (const char *fp = std::getenv("PBH_IID_PAIR")) e->iid_pair = std::atoi(fp) != 0;
   if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::min(20, std::max(0, std::atoi(fa)));
   if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
   if (const char *fs = std::getenv("PBH_FAIR_SHORT"))
@@ -986,6 +988,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.gmm_full = e->gmm_full ? 1 : 0;
   k.pair_full = e->pair_full ? 1 : 0;
   k.iid_full = e->iid_full ? 1 : 0;
+  k.iid_pair = e->iid_pair ? 1 : 0;
   k.fair = e->fair;
   k.pair_wg = e->bal ? 512 : e->pair_wg;
   k.bal = e->bal;

@@ -120,6 +120,7 @@ struct KArgs {
   int32_t gmm_full;    // the quad kernel's steady-state form is allowed
   int32_t pair_full;   // the lane-pair kernel's steady-state form is allowed
   int32_t iid_full;    // cfg1's steady-state iid-Normal form is allowed
+  int32_t iid_pair;    // ... on lane pairs (mh_iid_pair_kernel)
   int32_t fair;        // alternate the SIMD's wave priorities every 2^fair real-time ticks (0: off)
   int32_t pair_wg;     // FULL pair kernel's workgroup size (256 or 512)
   int32_t fair_rel;    // FULL pair kernel: the alternation clock starts at the wave's loop entry

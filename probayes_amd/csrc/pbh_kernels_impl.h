@@ -788,20 +788,32 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
   const double logC = a.norm_logC;
   const bool has_prior = a.has_prior != 0;
   const double prior_logp = a.prior_logp;
-  const uint32_t plo_incl = a.plo_incl, phi_incl = a.phi_incl;
+  // the prior box as closed limits (lo_closed / hi_closed: the same tests)
   double plo[D], phi[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    plo[k] = has_prior ? in_vgpr_f64(cld(a.plo, k)) : 0.;
-    phi[k] = has_prior ? in_vgpr_f64(cld(a.phi, k)) : 0.;
+    plo[k] = has_prior ? in_vgpr_f64(lo_closed(cld(a.plo, k), (a.plo_incl >> k) & 1u)) : 0.;
+    phi[k] = has_prior ? in_vgpr_f64(hi_closed(cld(a.phi, k), (a.phi_incl >> k) & 1u)) : 0.;
   }
   const uint32_t rowb = (uint32_t)(a.n * 8);
+  // the launch's records through three loop-invariant resources spanning
+  // them (iid_full_form: under kNoStore bytes), the record as the scalar
+  // offset; padding lanes' voff kNoStore fails the range check
+  const int64_t r0 = a.g0 - a.rec_base;
+  double *const tx0 = wave_uniform(a.tx + r0 * D * a.n);
+  double *const tl0 = wave_uniform(a.tlp + r0 * a.n);
+  double *const ta0 = wave_uniform(reinterpret_cast<double *>(a.tacc + r0 * a.W));
+  const uint32_t xspan = (uint32_t)(a.n_steps * D) * rowb;
+  const uint32_t lspan = (uint32_t)a.n_steps * rowb;
+  const uint32_t abytes = (uint32_t)(a.W * 8);
+  const uint32_t aspan = (uint32_t)a.n_steps * abytes;
+  uint32_t xoffk[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) xoffk[k] = active ? (uint32_t)(c * 8) + (uint32_t)k * rowb : kNoStore;
   const uint32_t xoff = active ? (uint32_t)(c * 8) : kNoStore;
   const uint32_t aoff = lane == 0 ? (uint32_t)((c >> 6) * 8) : kNoStore;
-  const uint32_t abytes = (uint32_t)(a.W * 8);
-  int64_t rec = a.g0 - a.rec_base;
   const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);   // SGPRs stay free
-  for (int s = 0; s < a.n_steps; ++s, ++rec) {
+  for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     // ---- draws: mh_kernel's production uniform draws ----
     double r[D];
@@ -860,13 +872,7 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
         // (x > lo) or (inclusive and x == lo): the reference's comparison
         uint64_t in = ~0ull;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          const uint64_t lo_ok = __ballot(xp[k] > plo[k]) |
-                                 (((plo_incl >> k) & 1u) ? __ballot(xp[k] == plo[k]) : 0ull);
-          const uint64_t hi_ok = __ballot(xp[k] < phi[k]) |
-                                 (((phi_incl >> k) & 1u) ? __ballot(xp[k] == phi[k]) : 0ull);
-          in &= lo_ok & hi_ok;
-        }
+        for (int k = 0; k < D; ++k) in &= __ballot(xp[k] >= plo[k]) & __ballot(xp[k] <= phi[k]);
         out = sel_f64(in, kNearlyNegInf, prior_logp) + out;
       }
       lpp = out;
@@ -887,14 +893,12 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
 #pragma unroll
     for (int k = 0; k < D; ++k) x[k] = sel_f64(accm, x[k], xp[k]);
     lp = sel_f64(accm, lp, lpp);
-    // ---- trace: record rec = step - rec_base ----
-    double *row = a.tx + rec * D * a.n;   // wave-uniform
+    // ---- trace: record g - rec_base = r0 + s ----
 #pragma unroll
-    for (int k = 0; k < D; ++k) st_buf_n(row + k * a.n, rowb, xoff, x[k]);
-    st_buf_n(a.tlp + rec * a.n, rowb, xoff, lp);
+    for (int k = 0; k < D; ++k) st_buf_ns(tx0, xspan, xoffk[k], (uint32_t)s * (D * rowb), x[k]);
+    st_buf_ns(tl0, lspan, xoff, (uint32_t)s * rowb, lp);
     const uint64_t am = accm & __ballot(active);
-    st_buf_n(reinterpret_cast<double *>(a.tacc + rec * a.W), abytes, aoff,
-             __builtin_bit_cast(double, am));
+    st_buf_ns(ta0, aspan, aoff, (uint32_t)s * abytes, __builtin_bit_cast(double, am));
   }
   if (active) {
 #pragma unroll
@@ -955,6 +959,196 @@ __device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
   const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
   ev = __builtin_bit_cast(double, (uint64_t)a[0] | ((uint64_t)b[0] << 32));
   od = __builtin_bit_cast(double, (uint64_t)a[1] | ((uint64_t)b[1] << 32));
+}
+
+// ---------------------------------------------------------------------------
+// cfg1's steady-state form on lane PAIRS (mh_iid_pair_kernel, the default
+// for iid_full_form).  One lane per chain leaves 65 536 chains at one
+// wavefront per SIMD, and a lone wavefront issues at most one instruction
+// per ~6 cycles: the step is issue- and latency-bound at half the SIMD's
+// rate.  Here chain c sits in both lanes l and l + 32 of a wavefront of 32
+// chains (2 048 wavefronts = 2 per SIMD).  The draws and the spherical delta
+// depend on no state, so they are split: for the step pair (2P, 2P + 1)
+// half h forms step 2P + h's Philox block, its uniforms, its 22-bit
+// threshold lead and its scaled delta (the sphere's rsq included), and two
+// v_permlane32_swap exchanges per double give both halves both steps'.
+// Both halves then run the state update (ufun, density, filter, selects) on
+// identical values, so every lane holds the chain's state.  The log of a
+// ufun dim of the state is carried: ln x' of the proposal is evaluated beside
+// the density and the decision instead of ln x at the next step's head (the
+// same function of the same value: the same bits).  Half 0 stores dim 0 and
+// the lp row, half 1 dim 1 (D = 2: one store instruction for both dims), and
+// each wavefront writes its 32-bit half of the record's 64-bit accept word.
+// The draws and arithmetic are mh_iid_full_kernel's: identical chains
+// (test_iid_pair_form_is_the_one_lane_form).
+// ---------------------------------------------------------------------------
+template <int D, int UFM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+void mh_iid_pair_kernel(KArgs a) {
+  static_assert(D >= 1 && D <= 2, "iid pair kernel: d <= 2");
+  __shared__ double s_bmt[kBm64Doubles];
+  const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int64_t wave = gt >> 6;
+  const int64_t c = wave * 32 + (lane & 31);
+  const bool active = c < a.n;
+  const int64_t cc = active ? c : 0;
+  const int64_t chain = a.off + cc;
+  double x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) x[k] = a.x[k * a.n + cc];
+  double lp = a.lp[cc];
+  double plen[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) plen[k] = cld(a.plen, k);
+  bm64_load(s_bmt, a.bm64);
+  __builtin_amdgcn_s_waitcnt(0);
+  const double d0 = a.sdelta;
+  const double beta = a.acc_beta;
+  const int i0 = a.i0, i1 = a.i1;
+  const double tw0 = cld(a.tw, 0), tw1 = cld(a.tw, 1), nobs = (double)a.tn;
+  const double logC = a.norm_logC;
+  const bool has_prior = a.has_prior != 0;
+  const double prior_logp = a.prior_logp;
+  // the prior box as closed limits (lo_closed / hi_closed: the same tests)
+  double plo[D], phi[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    plo[k] = has_prior ? in_vgpr_f64(lo_closed(cld(a.plo, k), (a.plo_incl >> k) & 1u)) : 0.;
+    phi[k] = has_prior ? in_vgpr_f64(hi_closed(cld(a.phi, k), (a.phi_incl >> k) & 1u)) : 0.;
+  }
+  double lx[D];   // ln x of the ufun dims of the state
+#pragma unroll
+  for (int k = 0; k < D; ++k) lx[k] = ((UFM >> k) & 1) ? ln_ufun(x[k], s_bmt) : 0.;
+  const uint32_t rowb = (uint32_t)(a.n * 8);
+  // stores: half 0 dim 0 + lp, half 1 dim 1 (a D = 1 chain: half 0 only)
+  const uint32_t xoff = active && (D == 2 || h == 0) ? (uint32_t)(h * a.n * 8 + c * 8) : kNoStore;
+  const uint32_t loff = active && h == 0 ? (uint32_t)(c * 8) : kNoStore;
+  const uint64_t hmask = 0xFFFFFFFF00000000ull;   // the lanes of half 1
+  // the accept word: lane 0 writes this wavefront's 32 bits of chains
+  // [64 w, 64 w + 64): the low or the high half of word w = c >> 6
+  // (the last wavefront of an odd count also zeroes the high half: lane 1)
+  const bool tail = (wave & 1) == 0 && 32 * (wave + 1) >= a.n;
+  const uint32_t aoff = lane == 0 ? (uint32_t)(wave * 4)
+                      : lane == 1 && tail ? (uint32_t)(wave * 4 + 4) : kNoStore;
+  const uint32_t amsk = lane == 1 ? 0u : ~0u;
+  const uint32_t abytes = (uint32_t)(a.W * 8);
+  const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);
+  const int64_t gend = a.g0 + a.n_steps;
+  const uint64_t actm = __ballot(active) & 0xFFFFFFFFull;
+  for (int64_t P = a.g0 >> 1; 2 * P < gend; ++P) {
+    // ---- this half's step of the pair: draws and the scaled delta ----
+    const int64_t gh = 2 * P + h;
+    double dl[D];
+    uint32_t lead;
+    {
+      const u32x4 w = philox4x32_10_rk(ctr(0, gh, chain), rk);
+      double r[D];
+      r[0] = u01(w.x, w.y);
+      if (D >= 2) r[D - 1] = u01(w.z, w.w);
+      lead = ((w.x & 31u) << 17) | ((w.y & 63u) << 11) |
+             (D >= 2 ? (((w.z & 31u) << 6) | (w.w & 63u)) : (w.z >> 21));
+      double sq[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        dl[k] = -d0 + (d0 - -d0) * r[k];
+        sq[k] = dl[k] * dl[k];
+      }
+      const double ss = np_sum_regs<D>(sq, D);
+      const double rq = rsq_nr(__builtin_fmax(ss, kNearlyPosZero));
+      const double sc = ss >= kNearlyPosZero ? d0 * rq : __builtin_inf();
+#pragma unroll
+      for (int k = 0; k < D; ++k) dl[k] = (dl[k] * sc) * plen[k];
+    }
+    double dls[2][D];
+    uint32_t leads[2];
+#pragma unroll
+    for (int k = 0; k < D; ++k) halves_f64(dl[k], dls[0][k], dls[1][k]);
+    {
+      const auto l2 = __builtin_amdgcn_permlane32_swap(lead, lead, false, false);
+      leads[0] = l2[0];
+      leads[1] = l2[1];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t g = 2 * P + j;
+      if (g < a.g0 || g >= gend) continue;   // wave-uniform: a launch's ends
+      double xp[D], lxp[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        lxp[k] = 0.;
+        if (((UFM >> k) & 1) != 0) {
+          lxp[k] = lx[k] + dls[j][k];
+          xp[k] = exp_ufun(lxp[k], s_bmt);
+        } else {
+          xp[k] = x[k] + dls[j][k];
+        }
+      }
+      // the proposal's ln x' (the next state's, if accepted): beside the
+      // density and the decision
+      double lnp[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) lnp[k] = ((UFM >> k) & 1) ? ln_ufun(xp[k], s_bmt) : 0.;
+      // joint_density<D, NORM_IID, FAST> (mh_iid_full_kernel's operations)
+      double lpp;
+      {
+        double mu = 0., sg = 1., l = 0.;
+        bool have = false;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          if (k == i0) mu = xp[k];
+          if (k == i1) sg = xp[k];
+          if (k == i1 && ((UFM >> k) & 1)) { l = lxp[k]; have = true; }
+        }
+        const double lsg = have ? l : fast_log(sg);
+        const double dm = tw0 - mu;
+        const double ssd = __builtin_fma(nobs * dm, dm, tw1);
+        const double s2 = sg * sg;
+        double ri = __builtin_amdgcn_rcp(s2);
+        ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+        ri = __builtin_fma(__builtin_fma(-s2, ri, 1.0), ri, ri);
+        double out = -0.5 * ssd * ri - nobs * (logC + lsg);
+        if (has_prior) {
+          uint64_t in = ~0ull;
+#pragma unroll
+          for (int k = 0; k < D; ++k) in &= __ballot(xp[k] >= plo[k]) & __ballot(xp[k] <= phi[k]);
+          out = sel_f64(in, kNearlyNegInf, prior_logp) + out;
+        }
+        lpp = out;
+      }
+      const double bA = lpp * beta, bB = lp * beta;
+      const DecisionMask dm = accept_filter_lead_mask<22>(bA, bB, leads[j], false);
+      uint64_t accm = dm.acc;
+      const uint64_t needm = dm.need & __ballot(true);
+      if (needm) {   // wave-uniform, rare: both halves of a chain agree
+        bool ex = false;
+        if (__builtin_amdgcn_inverse_ballot_w64(needm)) {
+          const u32x4 w = philox4x32_10(ctr(0xFFFFu, g, chain), a.seed_lo, a.seed_hi);
+          ex = ratio_accept(bA, bB, u01((leads[j] << 10) | (w.x >> 22), w.y), false, a.log_npi);
+        }
+        accm = (accm & ~needm) | (__ballot(ex) & needm);
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        x[k] = sel_f64(accm, x[k], xp[k]);
+        if ((UFM >> k) & 1) lx[k] = sel_f64(accm, lx[k], lnp[k]);
+      }
+      lp = sel_f64(accm, lp, lpp);
+      // ---- trace: record g - rec_base ----
+      const int64_t rec = g - a.rec_base;
+      double *row = a.tx + rec * D * a.n;   // wave-uniform
+      st_buf_n(row, (uint32_t)D * rowb, xoff, D == 2 ? sel_f64(hmask, x[0], x[D - 1]) : x[0]);
+      st_buf_n(a.tlp + rec * a.n, rowb, loff, lp);
+      st_buf32_n(reinterpret_cast<uint32_t *>(a.tacc + rec * a.W), abytes, aoff,
+                 (uint32_t)(accm & actm) & amsk);
+    }
+  }
+  if (active && h == 0) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
+    a.lp[c] = lp;
+  }
 }
 
 template <int L>
@@ -2163,7 +2357,9 @@ void mh_gmm_quad_kernel(KArgs a) {
         const float E32 = e32 + qperm_add_f32<kQuadXor2>(e32);
         const float tlo = qperm_f32<j * 85>(tlown);
         const float thi = tlo + kLw;
-        const uint64_t pinm = __ballot((E32 >= 0x1p-40f) & (E32 <= 0x1p40f));
+        // two compares straight into masks (a ballot of their AND would
+        // materialise the bool in a VGPR first)
+        const uint64_t pinm = __ballot(E32 >= 0x1p-40f) & __ballot(E32 <= 0x1p40f);
         const uint64_t inrm = rinm & sinm & pinm;
         const uint64_t af = __ballot(thi * ls32 <= E32 * 0.999992f);
         const uint64_t rf = __ballot(tlo * ls32 > E32 * 1.000008f);
@@ -3013,6 +3209,7 @@ inline bool iid_full_form(const KArgs &a) {
          a.has_pred && a.thin == 1 && a.pscale != PBH_PSCALE_LIN && a.tx != nullptr &&
          !a.has_tfun && a.vint == 0 && a.bnd_on == 0 && !a.moments &&
          a.ufun < (1u << a.d) && a.n * 8 <= (int64_t)kNoStore &&   // masked stores
+         (int64_t)a.n_steps * a.d * a.n * 8 <= (int64_t)kNoStore &&   // the launch's span
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }
 
@@ -3155,6 +3352,18 @@ hipError_t launch_mh_d(const KArgs &a, hipStream_t st, size_t lds) {
     }
     if (a.target == PBH_TARGET_NORM_IID && a.prop == PBH_PROP_SPHERE) {
       if constexpr (D <= 2) {
+        if (iid_full_form(a) && a.iid_pair && 2 * a.n * 8 <= (int64_t)kNoStore) {
+          // lane pairs: 32 chains per wavefront
+          const int64_t waves = (a.n + 31) / 32;
+          const dim3 grid((unsigned)((waves * 64 + kBlock - 1) / kBlock)), block(kBlock);
+          switch (a.ufun) {
+            case 0: pbh_launch((mh_iid_pair_kernel<D, 0>), grid, block, 0, st, a); break;
+            case 1: pbh_launch((mh_iid_pair_kernel<D, 1>), grid, block, 0, st, a); break;
+            case 2: pbh_launch((mh_iid_pair_kernel<D, 2>), grid, block, 0, st, a); break;
+            default: pbh_launch((mh_iid_pair_kernel<D, 3>), grid, block, 0, st, a); break;
+          }
+          return hipGetLastError();
+        }
         if (iid_full_form(a)) {
           const dim3 grid((unsigned)((a.n + kBlock - 1) / kBlock)), block(kBlock);
           switch (a.ufun) {

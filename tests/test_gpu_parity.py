@@ -472,18 +472,24 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
       assert np.array_equal(ma[k], mb[k]), k
 
 
-def test_iid_steady_state_form_is_the_general_form(monkeypatch):
-  """cfg1's steady-state launch (mh_iid_full_kernel: iid-Normal target,
-  spherical delta, ufun on sigma, uniform prior, e-tempered ratio form) is
-  bit-for-bit mh_kernel's general form (PBH_IID_FULL=0): a ragged chain
-  count (padding lanes write nothing), launches of 1 and 13 steps, chains
+@pytest.mark.parametrize('pair', ['1', '0'])
+@pytest.mark.parametrize('n', [4096 + 5, 37])
+def test_iid_steady_state_form_is_the_general_form(monkeypatch, pair, n):
+  """cfg1's steady-state launch (iid-Normal target, spherical delta, ufun on
+  sigma, uniform prior, e-tempered ratio form) -- on lane pairs
+  (mh_iid_pair_kernel, PBH_IID_PAIR=1, the default) or one lane per chain
+  (mh_iid_full_kernel) -- is bit-for-bit mh_kernel's general form
+  (PBH_IID_FULL=0): ragged chain counts (padding lanes write nothing; an odd
+  number of 32-chain wavefronts leaves the last accept word half-owned),
+  launches of 1 and 13 steps starting on either step of a pair, chains
   started outside the prior box (density -inf until they enter it)."""
   from probayes_amd import Engine
   spec = oracle.golden_spec('metrohast_norm1d')
-  n, t = 4096 + 5, 61
+  t = 61
   init = golden_init('metrohast_norm1d', n)
   init[::89, 1] = 30.   # sigma outside (5, 20)
   outs = {}
+  monkeypatch.setenv('PBH_IID_PAIR', pair)
   for full in ('1', '0'):
     monkeypatch.setenv('PBH_IID_FULL', full)
     eng = Engine(spec)
