@@ -47,8 +47,10 @@ struct pbh_engine {
   bool xo_seeded = false;
   // legacy NumPy RandomState per chain (pbh_legacy_seed)
   uint32_t *mt_key = nullptr;
-  bool mt_db = false;          // mt_key is [2][624][n] (double-buffered)
+  int mt_mode = 0;             // mt_key layout: 0 [624][n], 1 [2][624][n], 2 Mt4's
+                               // [4][20][n][32] (four chunked blocks)
   bool legacy_db = true;       // PBH_LEGACY_DB=0: the in-place state
+  bool legacy_k4 = true;       // PBH_LEGACY_K4=0: the round-3 double-buffered state
   bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
@@ -114,6 +116,9 @@ struct pbh_engine {
 };
 
 namespace {
+
+// words of legacy state per chain in each layout (pbh_engine.mt_mode)
+int64_t mt_words(int mode) { return mode == 2 ? 4 * 20 * 32 : mode == 1 ? 2 * 624 : 624; }
 
 thread_local std::string g_err;
 
@@ -245,6 +250,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *fo = std::getenv("PBH_FAIR_OFF")) e->fair_off = std::atoi(fo);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
+  if (const char *lk = std::getenv("PBH_LEGACY_K4")) e->legacy_k4 = std::atoi(lk) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
   // A/B switch for the markers' fences; default 0 = hipEventDefault)
   unsigned ev_flags = 0;
@@ -731,9 +737,13 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   const int64_t n = e->n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  e->mt_db = e->legacy_db;   // the state layout is fixed at seeding
+  // the state layout is fixed at seeding
+  // (Mt4's resources take 32-bit byte offsets: its state must span < 2^32 B)
+  e->mt_mode = !e->legacy_db ? 0
+               : (e->legacy_k4 && e->legacy_win && mt_words(2) * 4 * n < (int64_t(1) << 32)) ? 2
+                                                                                          : 1;
   e->mt_stale = false;
-  int rc = dalloc(e->mt_key, (size_t)(e->mt_db ? 2 : 1) * 624 * n);
+  int rc = dalloc(e->mt_key, (size_t)mt_words(e->mt_mode) * n);
   if (!rc) rc = dalloc(e->mt_pos, n);
   if (!rc) rc = dalloc(e->mt_has, n);
   if (!rc) rc = dalloc(e->mt_gauss, n);
@@ -744,7 +754,7 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   hipError_t err = hipMemcpy(dseeds, seeds, n * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (err == hipSuccess)
     err = pbh::launch_legacy_seed(e->mt_key, e->mt_pos, e->mt_gauss, e->mt_has,
-                                  dseeds, n, e->mt_db ? 1 : 0, e->stream);
+                                  dseeds, n, e->mt_mode, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   dfree(dseeds);
   if (err != hipSuccess)
@@ -786,7 +796,7 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   a.d = e->d; a.R = R; a.gibbs = e->has_gibbs ? 1 : 0;
   a.normal = (!e->has_gibbs && e->k.prop == PBH_PROP_GAUSS) ? 1 : 0;
   a.vardelta = (!e->has_gibbs && e->k.prop == PBH_PROP_VARDELTA) ? 1 : 0;
-  a.db = e->mt_db ? 1 : 0;
+  a.db = e->mt_mode;
   a.win = e->legacy_win ? 1 : 0;
   a.vmode = e->k.vmode;
   a.vdelta = e->k.pdel;
@@ -1201,7 +1211,7 @@ int pbh_set_chains(pbh_engine *e, const double *x, const double *lp,
 
 int pbh_legacy_state_words(pbh_engine *e, int64_t *words) {
   if (check_ptr(e, "engine") || check_ptr(words, "words")) return PBH_ERR_ARG;
-  *words = e->mt_key ? (e->mt_db ? 2 : 1) * 624 : 0;
+  *words = e->mt_key ? mt_words(e->mt_mode) : 0;
   return PBH_OK;
 }
 
@@ -1213,7 +1223,7 @@ int pbh_get_legacy_state(pbh_engine *e, uint32_t *key, int32_t *pos,
   if (!e->mt_key) return fail(PBH_ERR_STATE, "no legacy streams (pbh_legacy_seed)");
   if (e->mt_stale) return fail(PBH_ERR_STATE, "legacy state stale after pbh_restore");
   const int64_t n = e->n;
-  const size_t kw = (size_t)(e->mt_db ? 2 : 1) * 624 * n;
+  const size_t kw = (size_t)mt_words(e->mt_mode) * n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(key, e->mt_key, kw * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -1230,7 +1240,7 @@ int pbh_set_legacy_state(pbh_engine *e, const uint32_t *key, const int32_t *pos,
     return PBH_ERR_ARG;
   if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first (the layout)");
   const int64_t n = e->n;
-  const size_t kw = (size_t)(e->mt_db ? 2 : 1) * 624 * n;
+  const size_t kw = (size_t)mt_words(e->mt_mode) * n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(e->mt_key, key, kw * sizeof(uint32_t), hipMemcpyHostToDevice));

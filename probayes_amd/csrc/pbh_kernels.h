@@ -177,7 +177,8 @@ struct LegacyArgs {
   double *out;          // replay rows [n_steps][R][n]
   int64_t n, n_steps, step0;
   int32_t d, R, gibbs, normal;
-  int32_t db;           // double-buffered state [2][624][n] (legacy_gen_db)
+  int32_t db;           // 1: double-buffered state [2][624][n] (legacy_gen_db);
+                        // 2: four chunked blocks [4][20][n][32 words] (Mt4)
   int32_t win;          // with db: consume through the LDS window (Mt3)
   int32_t vardelta;     // VARDELTA: per-dim modes vmode, steps vdelta [d]
   uint64_t vmode;

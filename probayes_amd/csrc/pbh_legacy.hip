@@ -267,10 +267,71 @@ struct Mt2 {
 // of HIP's uint4 struct stayed in scratch)
 typedef uint32_t w4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void mt3_twist(w4 *key, int64_t n, int64_t c, int s) {
-  auto q = [&](int b, int i) -> w4 & { return key[((int64_t)b * kQ + i) * n + c]; };
+// a block -> the next block: ld(0, i) / ld(1, i) read quad i of the source /
+// destination block, st(i, v) writes quad i of the destination
+template <class L, class S>
+__device__ __forceinline__ void twist_ls(L ld, S st) {
   constexpr int kTB = 14;   // twist batch (56 = 4 x 14, 98 = 7 x 14)
-  const int d = s ^ 1;
+#pragma unroll
+  for (int i0 = 0; i0 < 56; i0 += kTB) {
+    w4 a[kTB + 1], h[kTB + 1];
+#pragma unroll
+    for (int u = 0; u <= kTB; ++u) {
+      a[u] = ld(0, i0 + u);
+      h[u] = ld(0, i0 + 99 + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kTB; ++u) {
+      w4 o;
+      o.x = h[u].y ^ mt_f(a[u].x, a[u].y);
+      o.y = h[u].z ^ mt_f(a[u].y, a[u].z);
+      o.z = h[u].w ^ mt_f(a[u].z, a[u].w);
+      o.w = h[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+      st(i0 + u, o);
+    }
+  }
+  {                                          // quad 56: words 224 .. 227
+    const w4 a = ld(0, 56), nx = ld(0, 57), h = ld(0, 155), d0 = ld(1, 0);
+    w4 o;
+    o.x = h.y ^ mt_f(a.x, a.y);              // src[621]
+    o.y = h.z ^ mt_f(a.y, a.z);              // src[622]
+    o.z = h.w ^ mt_f(a.z, a.w);              // src[623]
+    o.w = d0.x ^ mt_f(a.w, nx.x);            // dst[0]
+    st(56, o);
+  }
+#pragma unroll
+  for (int i0 = 57; i0 < kQ - 1; i0 += kTB) {
+    w4 a[kTB + 1], l[kTB + 1];
+#pragma unroll
+    for (int u = 0; u <= kTB; ++u) {
+      a[u] = ld(0, i0 + u);
+      l[u] = ld(1, i0 - 57 + u);
+    }
+#pragma unroll
+    for (int u = 0; u < kTB; ++u) {
+      w4 o;
+      o.x = l[u].y ^ mt_f(a[u].x, a[u].y);
+      o.y = l[u].z ^ mt_f(a[u].y, a[u].z);
+      o.z = l[u].w ^ mt_f(a[u].z, a[u].w);
+      o.w = l[u + 1].x ^ mt_f(a[u].w, a[u + 1].x);
+      st(i0 + u, o);
+    }
+  }
+  {                                          // quad 155: words 620 .. 623
+    const w4 a = ld(0, kQ - 1), d0 = ld(1, 0), d98 = ld(1, 98), d99 = ld(1, 99);
+    w4 o;
+    o.x = d98.y ^ mt_f(a.x, a.y);            // dst[393]
+    o.y = d98.z ^ mt_f(a.y, a.z);            // dst[394]
+    o.z = d98.w ^ mt_f(a.z, a.w);            // dst[395]
+    o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
+    st(kQ - 1, o);
+  }
+}
+
+// block in buffer s -> the next block in buffer d, quads addressed by q(b, i)
+template <class Q>
+__device__ __forceinline__ void twist_q(Q q, int s, int d) {
+  constexpr int kTB = 14;   // twist batch (56 = 4 x 14, 98 = 7 x 14)
   for (int i0 = 0; i0 < 56; i0 += kTB) {
     w4 a[kTB + 1], h[kTB + 1];
 #pragma unroll
@@ -323,6 +384,10 @@ __device__ __forceinline__ void mt3_twist(w4 *key, int64_t n, int64_t c, int s) 
     o.w = d99.x ^ mt_f(a.w, d0.x);           // dst[396], with the new dst[0]
     q(d, kQ - 1) = o;
   }
+}
+
+__device__ __forceinline__ void mt3_twist(w4 *key, int64_t n, int64_t c, int s) {
+  twist_q([&](int b, int i) -> w4 & { return key[((int64_t)b * kQ + i) * n + c]; }, s, s ^ 1);
 }
 
 // Mt3's rare refills (a launch's first two, and a step longer than the
@@ -532,6 +597,279 @@ struct Mt3 {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Mt4 (the default since round 4): FOUR blocks per chain in a chunked
+// layout, consumed through Mt3's LDS window.
+// Why: the lanes of a wave drift apart in the stream (the polar rejection
+// consumes a variable number of words: after 1 000 cfg2 steps the spread is
+// several hundred words), and with two buffers a lane can twist only between
+// flipping into a block and reaching its middle -- so the twist ran as
+// several partial-wave rounds per block, and the [quad][chain] layout made a
+// drifted lane's 16-byte reads and writes share 128-byte lines with lanes that
+// needed them at other times (profiles/r04p_leg: 2 487 VALU per wave-step,
+// 14.4 GB of HBM traffic per 250 cfg2-width steps against ~7 GB of data, the
+// time growing call after call with the drift).
+// Here each chain keeps its current block and up to three twisted blocks
+// after it (`ready`).  A twist round runs for the whole wave when any lane
+// has nothing ahead and is half-way through its block (or its window head is
+// about to enter the next block); every lane that is not full twists one
+// block further, so the leader sets the pace and the laggards bank blocks
+// (correct for any drift: a lane that reaches a block end with nothing ahead
+// twists alone, out of line).  Layout [4][20 chunks][n][8 quads] of uint4: a
+// block of 156 quads padded to 160, and a chunk is one 128-byte line per lane,
+// so the window's refills (whole chunks) and the twists move whole lines
+// whatever the other lanes' positions.
+// Packed state: pos | cb << 16 | ready << 18 (cb = the current block's buffer).
+// ---------------------------------------------------------------------------
+constexpr int kK4 = 4, kCh = 20;   // buffers; 8-quad chunks per (padded) block
+__device__ __forceinline__ w4 &k4q(w4 *key, int64_t n, int64_t c, int b, int i) {
+  return key[((int64_t)(b * kCh + (i >> 3)) * n + c) * 8 + (i & 7)];
+}
+// The twist through a raw buffer resource over the whole state (the engine
+// takes this layout only while it spans < 2^32 bytes): each lane's source and
+// destination buffers are one per-lane byte offset each, and every quad's
+// chunk and position a uniform offset -- no per-load 64-bit address
+// arithmetic (with plain pointers the compiler spent ~8 VALU per load on
+// (b 20 + chunk) n + c).
+__device__ __forceinline__ void mt4_twist(w4 *key, int64_t n, int64_t c, int s, int d) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(key, 0, -1, 0x00020000);
+  const uint32_t plane = (uint32_t)n * 128u;   // one chunk of every chain
+  const uint32_t vs = (uint32_t)c * 128u + (uint32_t)(s * kCh) * plane;
+  const uint32_t vd = (uint32_t)c * 128u + (uint32_t)(d * kCh) * plane;
+  auto off = [&](int i) { return (uint32_t)(i >> 3) * plane + (uint32_t)(i & 7) * 16u; };
+  twist_ls(
+      [&](int b, int i) -> w4 {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(b ? vd : vs), (int)off(i), 0);
+        return w4{v.x, v.y, v.z, v.w};
+      },
+      [&](int i, w4 v) {
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rs, (int)vd, (int)off(i), 0);
+      });
+}
+// a lane that needs a block nobody twisted for it (out of line, rare)
+__device__ __attribute__((noinline)) void mt4_twist_cold(w4 *key, int64_t n, int64_t c,
+                                                         int s, int d) {
+  mt4_twist(key, n, c, s, d);
+}
+// stage the chunk at stream quad hq (launch-relative; block hq / 156) into
+// the ring; returns the number of quads staged (8, or 4 for a block's last)
+__device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win, int kw,
+                                         int b, int hc, int hq) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(key, 0, -1, 0x00020000);
+  const uint32_t vo = ((uint32_t)(b * kCh + hc) * (uint32_t)n + (uint32_t)c) * 128u;
+  w4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {   // one line
+    const v4u t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, u * 16, 0);
+    v[u] = w4{t.x, t.y, t.z, t.w};
+  }
+  const int nq = hc == kCh - 1 ? 4 : 8;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (u < nq) win[((hq + u) & (kw - 1)) * kBlockLegacy] = v[u];
+  return nq;
+}
+// the rare refills (a launch's first, a step longer than the window) out of
+// line; the head's block is twisted first if nothing has (values in and out:
+// returns hq | ready << 24)
+template <int H>
+__device__ __attribute__((noinline)) int mt4_refill_cold(w4 *key, int64_t n, int64_t c,
+                                                         w4 *win, int hq, int blk, int cb,
+                                                         int ready) {
+#pragma unroll 1
+  for (int k = 0; k < H / 8; ++k) {
+    const int hb = hq / kQ, hc = (hq - hb * kQ) >> 3;
+    if (hb - blk > ready) {   // the head's block is not twisted yet
+      mt4_twist_cold(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
+      ++ready;
+    }
+    hq += mt4_stage(key, n, c, win, 2 * H, (cb + hb - blk) & 3, hc, hq);
+  }
+  return hq | (ready << 24);
+}
+
+template <int H>
+struct Mt4 {
+  static constexpr bool kLockstep = true;
+  static constexpr bool kPeek = true;   // attempts2 / advance
+  static constexpr int kRefill = 312;
+  static constexpr int kW = 2 * H;      // window quads per lane (a power of two)
+  static_assert(H % 8 == 0, "whole chunks per refill");
+  w4 *key;
+  int64_t n, c;
+  int pos, cb, ready;
+  int blk;      // launch-relative block of pos
+  int hq;       // launch-relative stream quad (blk * 156 + quad) the head stages next
+  int hb, hc;   // the head's launch-relative block and chunk
+  w4 cur;
+  w4 *win;      // this lane's slot 0 (slot stride blockDim.x)
+
+  __device__ __forceinline__ w4 &slot(int k) {
+    return win[(k & (kW - 1)) * kBlockLegacy];
+  }
+  __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
+
+  __device__ __forceinline__ void refill_cold() {
+    const int r = mt4_refill_cold<H>(key, n, c, win, hq, blk, cb, ready);
+    hq = r & 0xFFFFFF;
+    ready = r >> 24;
+    hb = hq / kQ;
+    hc = (hq - hb * kQ) >> 3;
+  }
+
+  __device__ __forceinline__ void init(int st, w4 *w) {
+    pos = st & 0xFFFF;
+    cb = (st >> 16) & 3;
+    ready = (st >> 18) & 3;
+    blk = 0;
+    win = w;
+    hb = 0;
+    hc = (pos >> 2) >> 3;   // the chunk holding pos (pos = 624: the last one)
+    hq = hc * 8;
+    refill_cold();
+    refill_cold();
+    if (pos & 3) cur = slot(aq());
+  }
+
+  // wave-uniform point (top of a step): a twist round, then the window
+  __device__ __forceinline__ void maintain() {
+    const bool due = ready == 0 && (pos >= kRefill || hb > blk || hc + H / 8 > kCh);
+    if (__builtin_amdgcn_ballot_w64(due)) {
+      if (ready < kK4 - 1) {   // every lane with a free buffer: one block further
+        mt4_twist(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
+        ++ready;
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(hq - aq() <= H)) {
+      if (hq - aq() <= H) {
+#pragma unroll
+        for (int k = 0; k < H / 8; ++k) {
+          hq += mt4_stage(key, n, c, win, kW, (cb + hb - blk) & 3, hc, hq);
+          if (++hc == kCh) {
+            hc = 0;
+            ++hb;
+          }
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void flip() {   // into the next block (pos = kN)
+    if (ready == 0) {   // nothing twisted ahead (a step longer than half a block)
+      mt4_twist_cold(key, n, c, cb, (cb + 1) & 3);
+      ready = 1;
+    }
+    cb = (cb + 1) & 3;
+    --ready;
+    pos = 0;
+    ++blk;
+  }
+
+  __device__ __forceinline__ static uint32_t temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+
+  __device__ __forceinline__ uint32_t next32() {
+    if (pos == kN) flip();
+    const int u = pos & 3;
+    if (u == 0) {
+      const int k = aq();
+      if (k >= hq) refill_cold();   // a step longer than the window (rare)
+      cur = slot(k);
+    }
+    ++pos;
+    return temper(u == 0 ? cur.x : (u == 1 ? cur.y : (u == 2 ? cur.z : cur.w)));
+  }
+
+  // random_sample's two words at once (as Mt3)
+  __device__ __forceinline__ double next_double() {
+    uint32_t wa, wb;
+    if (pos & 1) {
+      wa = next32();
+      wb = next32();
+    } else {
+      if (pos == kN) flip();
+      const bool lo = (pos & 3) == 0;
+      if (lo) {
+        const int k = aq();
+        if (k >= hq) refill_cold();
+        cur = slot(k);
+      }
+      pos += 2;
+      wa = temper(lo ? cur.x : cur.z);
+      wb = temper(lo ? cur.y : cur.w);
+    }
+    const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+
+  // two polar attempts read ahead without consuming (as Mt3): the stream's
+  // quads are contiguous in the ring across a block end
+  __device__ __forceinline__ void attempts2(double &x1a, double &x2a, double &x1b,
+                                            double &x2b) {
+    if (pos == kN) flip();
+    const int k = aq();
+    if (k + 2 >= hq) refill_cold();   // fewer than 3 quads staged (rare)
+    const w4 A = slot(k), B = slot(k + 1), C = slot(k + 2);
+    const bool lo = (pos & 3) == 0;
+    const uint32_t w0 = temper(lo ? A.x : A.z), w1 = temper(lo ? A.y : A.w);
+    const uint32_t w2 = temper(lo ? A.z : B.x), w3 = temper(lo ? A.w : B.y);
+    const uint32_t w4_ = temper(lo ? B.x : B.z), w5 = temper(lo ? B.y : B.w);
+    const uint32_t w6 = temper(lo ? B.z : C.x), w7 = temper(lo ? B.w : C.y);
+    auto dbl = [](uint32_t a, uint32_t b) {
+      const int32_t ai = (int32_t)(a >> 5), bi = (int32_t)(b >> 6);
+      return (ai * 67108864.0 + bi) / 9007199254740992.0;
+    };
+    x1a = 2.0 * dbl(w0, w1) - 1.0;
+    x2a = 2.0 * dbl(w2, w3) - 1.0;
+    x1b = 2.0 * dbl(w4_, w5) - 1.0;
+    x2b = 2.0 * dbl(w6, w7) - 1.0;
+  }
+
+  // consume nw (4 or 8) words read by attempts2
+  __device__ __forceinline__ void advance(int nw) {
+    pos += nw;
+    if (pos > kN) {   // (pos == kN flips lazily)
+      const int rest = pos - kN;
+      pos = kN;
+      flip();
+      pos = rest;
+    }
+    if (pos & 3) cur = slot(aq());
+  }
+
+  __device__ __forceinline__ int packed() const { return pos | (cb << 16) | (ready << 18); }
+};
+
+// Seeding for Mt4: init_genrand into buffer 0, the first twist into buffer 1;
+// the lane starts at word 0 of buffer 1 with nothing twisted ahead.
+__global__ __launch_bounds__(256) void mt_seed_k4_kernel(uint32_t *key, int32_t *pos,
+                                                         double *gauss, int32_t *has_gauss,
+                                                         const uint32_t *seeds, int64_t n) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  w4 *qk = reinterpret_cast<w4 *>(key);
+  uint32_t s = seeds[c];
+  for (int i = 0; i < kQ; ++i) {
+    w4 w;
+    w.x = s; s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(4 * i + 1);
+    w.y = s; s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(4 * i + 2);
+    w.z = s; s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(4 * i + 3);
+    w.w = s; s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(4 * i + 4);
+    k4q(qk, n, c, 0, i) = w;
+  }
+  mt4_twist(qk, n, c, 0, 1);
+  pos[c] = 0 | (1 << 16) | (0 << 18);
+  gauss[c] = 0.0;
+  has_gauss[c] = 0;
+}
+
 // legacy_gauss: polar method, second deviate cached across calls
 template <class M>
 __device__ __forceinline__ double legacy_gauss(M &m, double &gauss, int &has) {
@@ -606,10 +944,20 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
 constexpr int kModeAny = -1, kModeGibbs = 0, kModeVardelta = 1, kModeNormal = 2,
               kModeRaw = 3;
 
-template <class M, int MODE = kModeAny>
+// s_ord (the windowed kernels): order[j] n per draw j, staged in LDS at the
+// kernel's start.  Read from a.order, every row index was a vector load
+// whose s_waitcnt vmcnt(0) also waited for the step's earlier trace stores
+// to be acknowledged (gfx9's vmcnt counts stores too) -- ten store round
+// trips per cfg2 step; so was blockDim.x (an implicit-argument load).
+template <class M, int MODE = kModeAny, bool SORD = false>
 __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m,
-                                                double2 *stage = nullptr) {
+                                                double2 *stage = nullptr,
+                                                const uint32_t *s_ord = nullptr) {
   constexpr bool kAny = MODE == kModeAny;
+  auto ord = [&](int j) -> int64_t {
+    if constexpr (SORD) return (int64_t)s_ord[j];
+    else return (int64_t)a.order[j] * a.n;
+  };
   double gauss = a.gauss[c];
   int has = a.has_gauss[c];
   const int64_t rowlen = (int64_t)a.R * a.n;
@@ -654,7 +1002,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       has = __builtin_amdgcn_readfirstlane(has);
       int j0 = 0;
       if (has) {
-        row[(int64_t)a.order[0] * a.n] = gauss;
+        row[ord(0)] = gauss;
         has = 0;
         gauss = 0.0;
         j0 = 1;
@@ -672,14 +1020,14 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
             const double r2a = x1a * x1a + x2a * x2a;
             const double r2b = x1b * x1b + x2b * x2b;
             if (r2a < 1.0 && r2a != 0.0) {
-              stage[np * blockDim.x + threadIdx.x] = make_double2(x1a, x2a);
+              stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1a, x2a);
               ++np;
             }
             int used = 4;
             if (np < need) {
               used = 8;
               if (r2b < 1.0 && r2b != 0.0) {
-                stage[np * blockDim.x + threadIdx.x] = make_double2(x1b, x2b);
+                stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1b, x2b);
                 ++np;
               }
             }
@@ -693,7 +1041,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
             const double x2 = 2.0 * m.next_double() - 1.0;
             const double r2 = x1 * x1 + x2 * x2;
             if (r2 < 1.0 && r2 != 0.0) {
-              stage[np * blockDim.x + threadIdx.x] = make_double2(x1, x2);
+              stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1, x2);
               ++np;
             }
           }
@@ -703,13 +1051,13 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
 #pragma unroll 4
       for (int k = 0; k < kmax; ++k) {
         if (k < need) {
-          const double2 p = stage[k * blockDim.x + threadIdx.x];
+          const double2 p = stage[k * kBlockLegacy + threadIdx.x];
           const double r2 = p.x * p.x + p.y * p.y;
           const double f = sqrt(-2.0 * log(r2) / r2);
           const int j = j0 + 2 * k;
-          row[(int64_t)a.order[j] * a.n] = f * p.y;
+          row[ord(j)] = f * p.y;
           if (j + 1 < a.d) {
-            row[(int64_t)a.order[j + 1] * a.n] = f * p.x;
+            row[ord(j + 1)] = f * p.x;
           } else {
             gauss = f * p.x;   // cached for the next draw (odd d)
             has = 1;
@@ -722,7 +1070,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
     if constexpr (!kAny && MODE != kModeRaw) continue;   // not reached
     for (int j = 0; j < a.d; ++j) {
       const double v = (kAny && a.normal) ? legacy_gauss(m, gauss, has) : m.next_double();
-      row[(int64_t)a.order[j] * a.n] = v;    // draw j feeds dim order[j]
+      row[ord(j)] = v;    // draw j feeds dim order[j]
     }
     row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
   }
@@ -759,6 +1107,9 @@ template <int H, int MODE>
 __global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void legacy_gen_win_kernel(LegacyArgs a) {
   extern __shared__ w4 s_lw[];
+  __shared__ uint32_t s_ord[PBH_MAX_DIM];   // order[j] n (a multiple of 16 B)
+  if (!a.gibbs && threadIdx.x < (unsigned)a.d) s_ord[threadIdx.x] = (uint32_t)(a.order[threadIdx.x] * a.n);
+  __syncthreads();
   const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
   if (c >= a.n) return;
   Mt3<H> m;
@@ -766,8 +1117,47 @@ void legacy_gen_win_kernel(LegacyArgs a) {
   m.n = a.n;
   m.c = c;
   m.init(a.pos[c], s_lw + threadIdx.x);
-  legacy_gen_body<Mt3<H>, MODE>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy));
+  legacy_gen_body<Mt3<H>, MODE, true>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord);
   a.pos[c] = m.packed();
+}
+
+template <int H, int MODE>
+__global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void legacy_gen_k4_kernel(LegacyArgs a) {
+  extern __shared__ w4 s_lw[];
+  __shared__ uint32_t s_ord[PBH_MAX_DIM];   // order[j] n (a multiple of 16 B)
+  if (!a.gibbs && threadIdx.x < (unsigned)a.d) s_ord[threadIdx.x] = (uint32_t)(a.order[threadIdx.x] * a.n);
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
+  if (c >= a.n) return;
+  Mt4<H> m;
+  m.key = reinterpret_cast<w4 *>(a.key);
+  m.n = a.n;
+  m.c = c;
+  m.init(a.pos[c], s_lw + threadIdx.x);
+  legacy_gen_body<Mt4<H>, MODE, true>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord);
+  a.pos[c] = m.packed();
+}
+
+template <int H, int MODE>
+hipError_t launch_k4_mode(const LegacyArgs &a, hipStream_t s) {
+  const int pairs = a.normal ? (a.d + 1) / 2 : 0;
+  const size_t lds = (size_t)(2 * H + pairs) * kBlockLegacy * sizeof(uint4);
+  hipError_t err = hipFuncSetAttribute(
+      reinterpret_cast<const void *>(&legacy_gen_k4_kernel<H, MODE>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  const dim3 grid((unsigned)((a.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+  hipLaunchKernelGGL((legacy_gen_k4_kernel<H, MODE>), grid, block, lds, s, a);
+  return hipGetLastError();
+}
+
+template <int H>
+hipError_t launch_k4(const LegacyArgs &a, hipStream_t s) {
+  if (a.gibbs) return launch_k4_mode<H, kModeGibbs>(a, s);
+  if (a.vardelta) return launch_k4_mode<H, kModeVardelta>(a, s);
+  if (a.normal) return launch_k4_mode<H, kModeNormal>(a, s);
+  return launch_k4_mode<H, kModeRaw>(a, s);
 }
 
 template <int H, int MODE>
@@ -797,7 +1187,10 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
                               int64_t n, int32_t db, hipStream_t s) {
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-  if (db)
+  if (db == 2)
+    hipLaunchKernelGGL(mt_seed_k4_kernel, grid, block, 0, s, key, pos, gauss,
+                       has_gauss, seeds, n);
+  else if (db)
     hipLaunchKernelGGL(mt_seed_db_kernel, grid, block, 0, s, key, pos, gauss,
                        has_gauss, seeds, n);
   else
@@ -807,6 +1200,10 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
 }
 
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
+  if (a.db == 2) {   // Mt4: four chunked blocks through the window
+    if (!a.normal || a.d <= 12) return launch_k4<16>(a, s);
+    return launch_k4<8>(a, s);
+  }
   if (a.db && a.win) {
     // 2H = 32 quads (128 words) per lane while the stage leaves room
     if (!a.normal || a.d <= 12) return launch_win<16>(a, s);
