@@ -654,22 +654,29 @@ __device__ __attribute__((noinline)) void mt4_twist_cold(w4 *key, int64_t n, int
 }
 // stage the chunk at stream quad hq (launch-relative; block hq / 156) into
 // the ring; returns the number of quads staged (8, or 4 for a block's last)
-__device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win, int kw,
-                                         int b, int hc, int hq) {
+__device__ __forceinline__ void mt4_load(w4 *key, int64_t n, int64_t c, int b, int hc,
+                                         w4 (&v)[8]) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(key, 0, -1, 0x00020000);
   const uint32_t vo = ((uint32_t)(b * kCh + hc) * (uint32_t)n + (uint32_t)c) * 128u;
-  w4 v[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {   // one line
     const v4u t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, u * 16, 0);
     v[u] = w4{t.x, t.y, t.z, t.w};
   }
+}
+__device__ __forceinline__ int mt4_put(w4 *win, int kw, int hc, int hq, const w4 (&v)[8]) {
   const int nq = hc == kCh - 1 ? 4 : 8;
 #pragma unroll
   for (int u = 0; u < 8; ++u)
     if (u < nq) win[((hq + u) & (kw - 1)) * kBlockLegacy] = v[u];
   return nq;
+}
+__device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win, int kw,
+                                         int b, int hc, int hq) {
+  w4 v[8];
+  mt4_load(key, n, c, b, hc, v);
+  return mt4_put(win, kw, hc, hq, v);
 }
 // the rare refills (a launch's first, a step longer than the window) out of
 // line; the head's block is twisted first if nothing has (values in and out:
@@ -705,6 +712,10 @@ struct Mt4 {
   int hb, hc;   // the head's launch-relative block and chunk
   w4 cur;
   w4 *win;      // this lane's slot 0 (slot stride blockDim.x)
+  // the next refill's chunks, loaded one refill ahead (pf): their loads
+  // complete during the steps in between instead of stalling the step top
+  w4 pfv[H / 8][8];
+  bool pf;
 
   __device__ __forceinline__ w4 &slot(int k) {
     return win[(k & (kW - 1)) * kBlockLegacy];
@@ -717,6 +728,35 @@ struct Mt4 {
     ready = r >> 24;
     hb = hq / kQ;
     hc = (hq - hb * kQ) >> 3;
+    pf = false;   // the head moved: a prefetched refill is stale
+  }
+
+  // the next refill's blocks are twisted
+  __device__ __forceinline__ bool ahead_ok() const {
+    return (hb - blk) + (hc + H / 8 > kCh ? 1 : 0) <= ready;
+  }
+  __device__ __forceinline__ void prefetch() {
+    int b = hb, ch = hc;
+#pragma unroll
+    for (int k = 0; k < H / 8; ++k) {
+      mt4_load(key, n, c, (cb + b - blk) & 3, ch, pfv[k]);
+      if (++ch == kCh) {
+        ch = 0;
+        ++b;
+      }
+    }
+    pf = true;
+  }
+  __device__ __forceinline__ void commit() {
+#pragma unroll
+    for (int k = 0; k < H / 8; ++k) {
+      hq += mt4_put(win, kW, hc, hq, pfv[k]);
+      if (++hc == kCh) {
+        hc = 0;
+        ++hb;
+      }
+    }
+    pf = false;
   }
 
   __device__ __forceinline__ void init(int st, w4 *w) {
@@ -726,6 +766,7 @@ struct Mt4 {
     blk = 0;
     win = w;
     hb = 0;
+    pf = false;
     hc = (pos >> 2) >> 3;   // the chunk holding pos (pos = 624: the last one)
     hq = hc * 8;
     refill_cold();
@@ -744,15 +785,13 @@ struct Mt4 {
     }
     if (__builtin_amdgcn_ballot_w64(hq - aq() <= H)) {
       if (hq - aq() <= H) {
-#pragma unroll
-        for (int k = 0; k < H / 8; ++k) {
-          hq += mt4_stage(key, n, c, win, kW, (cb + hb - blk) & 3, hc, hq);
-          if (++hc == kCh) {
-            hc = 0;
-            ++hb;
-          }
-        }
+        if (!pf) prefetch();   // not loaded ahead (its block was not twisted then)
+        commit();
       }
+    }
+    // the next refill, ahead (whenever its blocks are twisted)
+    if (__builtin_amdgcn_ballot_w64(!pf && ahead_ok())) {
+      if (!pf && ahead_ok()) prefetch();
     }
   }
 
@@ -1047,22 +1086,43 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
           }
         }
       }
-      const int kmax = (a.d + 1) / 2;
-#pragma unroll 4
-      for (int k = 0; k < kmax; ++k) {
-        if (k < need) {
-          const double2 p = stage[k * kBlockLegacy + threadIdx.x];
-          const double r2 = p.x * p.x + p.y * p.y;
-          const double f = sqrt(-2.0 * log(r2) / r2);
-          const int j = j0 + 2 * k;
-          row[ord(j)] = f * p.y;
-          if (j + 1 < a.d) {
-            row[ord(j + 1)] = f * p.x;
-          } else {
-            gauss = f * p.x;   // cached for the next draw (odd d)
-            has = 1;
-          }
-        }
+      // the pairs' transcendental part, two independent pairs per
+      // iteration (one basic block: the scheduler interleaves their log /
+      // division / square-root chains); a last pair whose second deviate is
+      // cached (odd d - j0) after them
+      const int half = (a.d - j0) & 1;
+      const int nfull = need - half;
+      auto polar = [&](int k, double &g0, double &g1) {
+        const double2 p = stage[k * kBlockLegacy + threadIdx.x];
+        const double r2 = p.x * p.x + p.y * p.y;
+        const double f = sqrt(-2.0 * log(r2) / r2);
+        g0 = f * p.y;
+        g1 = f * p.x;
+      };
+      int k = 0;
+      for (; k + 2 <= nfull; k += 2) {
+        double a0, a1, b0, b1;
+        polar(k, a0, a1);
+        polar(k + 1, b0, b1);
+        const int j = j0 + 2 * k;
+        row[ord(j)] = a0;
+        row[ord(j + 1)] = a1;
+        row[ord(j + 2)] = b0;
+        row[ord(j + 3)] = b1;
+      }
+      if (k < nfull) {
+        double a0, a1;
+        polar(k, a0, a1);
+        row[ord(j0 + 2 * k)] = a0;
+        row[ord(j0 + 2 * k + 1)] = a1;
+        ++k;
+      }
+      if (half) {
+        double a0, a1;
+        polar(k, a0, a1);
+        row[ord(j0 + 2 * k)] = a0;
+        gauss = a1;   // cached for the next draw (odd d)
+        has = 1;
       }
       row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
       continue;
