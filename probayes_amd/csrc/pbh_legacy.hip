@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *po
 struct Mt {
   static constexpr bool kLockstep = false;
   static constexpr bool kPeek = false;
+  static constexpr bool kPeek4 = false;
   uint32_t *key;
   int64_t n, c;
   int pos;
@@ -142,6 +143,7 @@ __device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b) {
 struct Mt2 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = false;
+  static constexpr bool kPeek4 = false;
   static constexpr int kRefill = 312;
   uint4 *key;
   int64_t n, c;
@@ -418,6 +420,7 @@ template <int H>
 struct Mt3 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = true;   // attempts2 / advance
+  static constexpr bool kPeek4 = false;
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;   // window quads per lane (a power of two)
   static constexpr int kTB = 14;     // twist batch (56 = 4 x 14, 98 = 7 x 14)
@@ -665,23 +668,49 @@ __device__ __forceinline__ void mt4_load(w4 *key, int64_t n, int64_t c, int b, i
     v[u] = w4{t.x, t.y, t.z, t.w};
   }
 }
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+// random_sample of two raw words (tempered here)
+__device__ __forceinline__ double mt_dbl(uint32_t wa, uint32_t wb) {
+  const int32_t a = (int32_t)(mt_temper(wa) >> 5), b = (int32_t)(mt_temper(wb) >> 6);
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+// DBL: the ring holds each quad as the two random_sample doubles of its
+// word pairs (every draw of the Normal / Raw / Gibbs streams is a double at
+// an even position), tempered and converted once per word as the quad is
+// staged instead of at every read-ahead of the lockstep attempts
+template <bool DBL>
 __device__ __forceinline__ int mt4_put(w4 *win, int kw, int hc, int hq, const w4 (&v)[8]) {
   const int nq = hc == kCh - 1 ? 4 : 8;
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (u < nq) win[((hq + u) & (kw - 1)) * kBlockLegacy] = v[u];
+  for (int u = 0; u < 8; ++u) {
+    if (u < nq) {
+      if constexpr (DBL) {
+        const double2 d{mt_dbl(v[u].x, v[u].y), mt_dbl(v[u].z, v[u].w)};
+        reinterpret_cast<double2 *>(win)[((hq + u) & (kw - 1)) * kBlockLegacy] = d;
+      } else {
+        win[((hq + u) & (kw - 1)) * kBlockLegacy] = v[u];
+      }
+    }
+  }
   return nq;
 }
+template <bool DBL>
 __device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win, int kw,
                                          int b, int hc, int hq) {
   w4 v[8];
   mt4_load(key, n, c, b, hc, v);
-  return mt4_put(win, kw, hc, hq, v);
+  return mt4_put<DBL>(win, kw, hc, hq, v);
 }
 // the rare refills (a launch's first, a step longer than the window) out of
 // line; the head's block is twisted first if nothing has (values in and out:
 // returns hq | ready << 24)
-template <int H>
+template <int H, bool DBL>
 __device__ __attribute__((noinline)) int mt4_refill_cold(w4 *key, int64_t n, int64_t c,
                                                          w4 *win, int hq, int blk, int cb,
                                                          int ready) {
@@ -692,15 +721,16 @@ __device__ __attribute__((noinline)) int mt4_refill_cold(w4 *key, int64_t n, int
       mt4_twist_cold(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
       ++ready;
     }
-    hq += mt4_stage(key, n, c, win, 2 * H, (cb + hb - blk) & 3, hc, hq);
+    hq += mt4_stage<DBL>(key, n, c, win, 2 * H, (cb + hb - blk) & 3, hc, hq);
   }
   return hq | (ready << 24);
 }
 
-template <int H>
+template <int H, bool DBL = false>
 struct Mt4 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = true;   // attempts2 / advance
+  static constexpr bool kPeek4 = DBL;   // attempts4 (four attempts per iteration)
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;      // window quads per lane (a power of two)
   static_assert(H % 8 == 0, "whole chunks per refill");
@@ -723,7 +753,7 @@ struct Mt4 {
   __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
 
   __device__ __forceinline__ void refill_cold() {
-    const int r = mt4_refill_cold<H>(key, n, c, win, hq, blk, cb, ready);
+    const int r = mt4_refill_cold<H, DBL>(key, n, c, win, hq, blk, cb, ready);
     hq = r & 0xFFFFFF;
     ready = r >> 24;
     hb = hq / kQ;
@@ -750,7 +780,7 @@ struct Mt4 {
   __device__ __forceinline__ void commit() {
 #pragma unroll
     for (int k = 0; k < H / 8; ++k) {
-      hq += mt4_put(win, kW, hc, hq, pfv[k]);
+      hq += mt4_put<DBL>(win, kW, hc, hq, pfv[k]);
       if (++hc == kCh) {
         hc = 0;
         ++hb;
@@ -815,6 +845,7 @@ struct Mt4 {
   }
 
   __device__ __forceinline__ uint32_t next32() {
+    static_assert(!DBL, "the staged-double ring holds no raw words");
     if (pos == kN) flip();
     const int u = pos & 3;
     if (u == 0) {
@@ -826,26 +857,40 @@ struct Mt4 {
     return temper(u == 0 ? cur.x : (u == 1 ? cur.y : (u == 2 ? cur.z : cur.w)));
   }
 
-  // random_sample's two words at once (as Mt3)
+  __device__ __forceinline__ const double2 &dslot(int k) {
+    return reinterpret_cast<const double2 *>(win)[(k & (kW - 1)) * kBlockLegacy];
+  }
+
+  // random_sample's two words at once (as Mt3); DBL: the staged double
   __device__ __forceinline__ double next_double() {
-    uint32_t wa, wb;
-    if (pos & 1) {
-      wa = next32();
-      wb = next32();
-    } else {
+    if constexpr (DBL) {   // positions are even
       if (pos == kN) flip();
-      const bool lo = (pos & 3) == 0;
-      if (lo) {
-        const int k = aq();
-        if (k >= hq) refill_cold();
-        cur = slot(k);
-      }
+      const int k = aq();
+      if (k >= hq) refill_cold();
+      const double2 d = dslot(k);
+      const double r = (pos & 2) ? d.y : d.x;
       pos += 2;
-      wa = temper(lo ? cur.x : cur.z);
-      wb = temper(lo ? cur.y : cur.w);
+      return r;
+    } else {
+      uint32_t wa, wb;
+      if (pos & 1) {
+        wa = next32();
+        wb = next32();
+      } else {
+        if (pos == kN) flip();
+        const bool lo = (pos & 3) == 0;
+        if (lo) {
+          const int k = aq();
+          if (k >= hq) refill_cold();
+          cur = slot(k);
+        }
+        pos += 2;
+        wa = temper(lo ? cur.x : cur.z);
+        wb = temper(lo ? cur.y : cur.w);
+      }
+      const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
+      return (a * 67108864.0 + b) / 9007199254740992.0;
     }
-    const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
-    return (a * 67108864.0 + b) / 9007199254740992.0;
   }
 
   // two polar attempts read ahead without consuming (as Mt3): the stream's
@@ -871,7 +916,25 @@ struct Mt4 {
     x2b = 2.0 * dbl(w6, w7) - 1.0;
   }
 
-  // consume nw (4 or 8) words read by attempts2
+  // DBL: four polar attempts read ahead without consuming (words pos ..
+  // pos + 15, pos even: four slots, or five when pos is 2 mod 4), as 2 d - 1
+  __device__ __forceinline__ void attempts4(double (&x1)[4], double (&x2)[4]) {
+    if (pos == kN) flip();
+    const int k = aq();
+    if (k + 4 >= hq) refill_cold();   // fewer than 5 quads staged (rare)
+    const double2 A = dslot(k), B = dslot(k + 1), C = dslot(k + 2), D = dslot(k + 3),
+                  E = dslot(k + 4);
+    const bool lo = (pos & 3) == 0;
+    const double d[8] = {lo ? A.x : A.y, lo ? A.y : B.x, lo ? B.x : B.y, lo ? B.y : C.x,
+                         lo ? C.x : C.y, lo ? C.y : D.x, lo ? D.x : D.y, lo ? D.y : E.x};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x1[i] = 2.0 * d[2 * i] - 1.0;
+      x2[i] = 2.0 * d[2 * i + 1] - 1.0;
+    }
+  }
+
+  // consume nw (a multiple of 4, <= 16) words read by attempts2 / attempts4
   __device__ __forceinline__ void advance(int nw) {
     pos += nw;
     if (pos > kN) {   // (pos == kN flips lazily)
@@ -880,7 +943,8 @@ struct Mt4 {
       flip();
       pos = rest;
     }
-    if (pos & 3) cur = slot(aq());
+    if constexpr (!DBL)
+      if (pos & 3) cur = slot(aq());
   }
 
   __device__ __forceinline__ int packed() const { return pos | (cb << 16) | (ready << 18); }
@@ -1012,19 +1076,21 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
         row[(int64_t)j * a.n] = j < cnt ? m.next_double() : __builtin_nan("");
       continue;
     }
-    if ((kAny || MODE == kModeVardelta) && (!kAny || a.vardelta)) {
-      // Field.eval_delta draws per variable in key order (variable.py:618-633)
-      for (int j = 0; j < a.d; ++j) {
-        const int md = (int)((a.vmode >> (2 * j)) & 3u);
-        double v = __builtin_nan("");
-        if (md == PBH_VAR_RANDINT)
-          v = legacy_randint(m, a.vdelta[j]);
-        else if (md != PBH_VAR_FIXED)
-          v = m.next_double();
-        row[(int64_t)j * a.n] = v;
+    if constexpr (kAny || MODE == kModeVardelta) {
+      if (!kAny || a.vardelta) {
+        // Field.eval_delta draws per variable in key order (variable.py:618-633)
+        for (int j = 0; j < a.d; ++j) {
+          const int md = (int)((a.vmode >> (2 * j)) & 3u);
+          double v = __builtin_nan("");
+          if (md == PBH_VAR_RANDINT)
+            v = legacy_randint(m, a.vdelta[j]);
+          else if (md != PBH_VAR_FIXED)
+            v = m.next_double();
+          row[(int64_t)j * a.n] = v;
+        }
+        row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
+        continue;
       }
-      row[(int64_t)a.d * a.n] = m.next_double();   // the MH threshold
-      continue;
     }
     if (M::kLockstep && (kAny || MODE == kModeNormal) && (!kAny || a.normal)) {
       // the step's d polar-method normals.  Lanes run the ATTEMPTS in
@@ -1048,7 +1114,29 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       }
       const int need = (a.d - j0 + 1) / 2;   // pairs this lane draws
       int np = 0;
-      if constexpr (M::kPeek) {
+      if constexpr (M::kPeek && M::kPeek4) {
+        // four attempts per lockstep iteration from the staged doubles
+        // (~3 iterations for 5 pairs), consumed only as far as they are used
+        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+          if (np < need) {
+            double x1[4], x2[4];
+            m.attempts4(x1, x2);
+            int used = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const double r2 = x1[i] * x1[i] + x2[i] * x2[i];
+              if (np < need) {
+                used += 4;
+                if (r2 < 1.0 && r2 != 0.0) {
+                  stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1[i], x2[i]);
+                  ++np;
+                }
+              }
+            }
+            m.advance(used);
+          }
+        }
+      } else if constexpr (M::kPeek) {
         // two attempts per lockstep iteration (read ahead from the window,
         // consumed only as far as they are used): ~5.5 iterations for 5
         // pairs instead of ~9.5, and two independent chains of arithmetic
@@ -1190,12 +1278,13 @@ void legacy_gen_k4_kernel(LegacyArgs a) {
   __syncthreads();
   const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
   if (c >= a.n) return;
-  Mt4<H> m;
+  // the staged-double ring for every stream of double draws (not randint's words)
+  Mt4<H, MODE != kModeVardelta && MODE != kModeAny> m;
   m.key = reinterpret_cast<w4 *>(a.key);
   m.n = a.n;
   m.c = c;
   m.init(a.pos[c], s_lw + threadIdx.x);
-  legacy_gen_body<Mt4<H>, MODE, true>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord);
+  legacy_gen_body<Mt4<H, MODE != kModeVardelta && MODE != kModeAny>, MODE, true>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord);
   a.pos[c] = m.packed();
 }
 
