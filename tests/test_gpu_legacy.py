@@ -159,3 +159,24 @@ def test_device_streams_many_short_launches(name):
   one = eng.get_replay(0, total)
   eng.close()
   _check(one, ref, normal)
+
+
+@pytest.mark.parametrize('name', ['diag10', 'gauss5_permuted'])
+def test_device_streams_long_drift(name):
+  """Thousands of steps: the lanes of a wave drift hundreds of words apart
+  in their streams, so the four-block generator's laggards bank twisted
+  blocks (up to three ahead) while the leader sets the twist rounds, and
+  launches start and end anywhere in a block; every chain still draws its
+  own RandomState stream."""
+  spec = _specs()[name]
+  n = 96                                 # a full and a partial wavefront
+  seeds = np.arange(77_000, 77_000 + n)
+  sizes = [1000, 7, 1493]
+  eng = _engine(spec, n, seeds)
+  parts = []
+  for t in sizes:
+    eng.legacy_replay(t)
+    parts.append(eng.get_replay(0, t))
+  eng.close()
+  ref = oracle.legacy_streams(spec, seeds, sum(sizes))
+  _check(np.concatenate(parts), ref, set(range(int(spec['dim']))))
