@@ -586,6 +586,18 @@ hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
 // {-2 ln c_j, 1 / c_j} for c_j = (1024 + j) / 2048, j = 0..1024; then
 // 2^(i/64), i = 0..63.  Evaluated in long double (64-bit significand) and
 // rounded once to double.
+void legacy_log_table(double *out) {
+  for (int j = 0; j < kLegLogN; ++j) {
+    const long double c = 0.5L + (long double)j / 256.0L;   // exact
+    const long double t = logl(c);
+    const double hi = (double)(roundl(t * 4294967296.0L) / 4294967296.0L);   // k 2^-32
+    out[2 * j] = hi;
+    out[2 * j + 1] = (double)(t - (long double)hi);
+    out[kLegLogInv + j] = (double)(1.0L / c);
+  }
+  out[kLegLogDoubles - 1] = 0.0;
+}
+
 void bm64_tables(double *out) {
   double *lg = out + kBm64LogOff;
   for (int j = 0; j < kBm64LogN; ++j) {

@@ -70,6 +70,7 @@ struct pbh_engine {
   int64_t mom_steps = 0;
   // production fp64 normal tables (bm64, pbh_device.h), read into LDS
   double *bm64 = nullptr;
+  double *lgtab = nullptr;     // legacy_log_table (device legacy streams)
   double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
   bool spin_sync = true;     // poll <= 2 ms, then block; PBH_SYNC=block: block
   bool sync_event = false;   // PBH_SYNC=event: poll the last run's end event
@@ -288,7 +289,7 @@ int pbh_destroy(pbh_engine *e) {
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
-  dfree(e->bm64); dfree(e->ess);
+  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -801,6 +802,14 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   a.win = e->legacy_win ? 1 : 0;
   a.vmode = e->k.vmode;
   a.vdelta = e->k.pdel;
+  if (!e->lgtab) {
+    std::vector<double> lt(pbh::kLegLogDoubles);
+    pbh::legacy_log_table(lt.data());
+    rc = dalloc(e->lgtab, lt.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(e->lgtab, lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  a.lgtab = e->lgtab;
   hipError_t err = pbh::launch_legacy_gen(a, e->stream);
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   if (err != hipSuccess)

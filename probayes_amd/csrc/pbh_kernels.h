@@ -167,6 +167,11 @@ hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             hipStream_t st, bool fft = true);
 // Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
 void bm64_tables(double *out);
+// the legacy generator's log table (pbh_legacy.hip log_leg): 129 rows of
+// {ln c_j rounded to a multiple of 2^-32, the remainder}, then 1 / c_j, for
+// c_j = 1/2 + j/256; kLegLogDoubles doubles (a multiple of two)
+constexpr int kLegLogN = 129, kLegLogInv = 2 * kLegLogN, kLegLogDoubles = 3 * kLegLogN + 1;
+void legacy_log_table(double *out);
 // Legacy (NumPy RandomState) stream generation (pbh_legacy.hip).
 struct LegacyArgs {
   uint32_t *key;        // MT19937 words [624][n]
@@ -183,6 +188,7 @@ struct LegacyArgs {
   int32_t vardelta;     // VARDELTA: per-dim modes vmode, steps vdelta [d]
   uint64_t vmode;
   const double *vdelta;
+  const double *lgtab;  // legacy_log_table (Mt4's polar log)
 };
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,

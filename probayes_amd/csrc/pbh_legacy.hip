@@ -50,6 +50,7 @@ struct Mt {
   static constexpr bool kLockstep = false;
   static constexpr bool kPeek = false;
   static constexpr bool kPeek4 = false;
+  static constexpr bool kLogTab = false;
   uint32_t *key;
   int64_t n, c;
   int pos;
@@ -144,6 +145,7 @@ struct Mt2 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = false;
   static constexpr bool kPeek4 = false;
+  static constexpr bool kLogTab = false;
   static constexpr int kRefill = 312;
   uint4 *key;
   int64_t n, c;
@@ -421,6 +423,7 @@ struct Mt3 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = true;   // attempts2 / advance
   static constexpr bool kPeek4 = false;
+  static constexpr bool kLogTab = false;
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;   // window quads per lane (a power of two)
   static constexpr int kTB = 14;     // twist batch (56 = 4 x 14, 98 = 7 x 14)
@@ -731,6 +734,7 @@ struct Mt4 {
   static constexpr bool kLockstep = true;
   static constexpr bool kPeek = true;   // attempts2 / advance
   static constexpr bool kPeek4 = DBL;   // attempts4 (four attempts per iteration)
+  static constexpr bool kLogTab = true;  // the polar log from log_leg's table
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;      // window quads per lane (a power of two)
   static_assert(H % 8 == 0, "whole chunks per refill");
@@ -1047,6 +1051,36 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
 constexpr int kModeAny = -1, kModeGibbs = 0, kModeVardelta = 1, kModeNormal = 2,
               kModeRaw = 3;
 
+// log(x) of the polar method's r2 in (0, 1) (a normal double) for Mt4
+// (Tang's table method): x = m 2^e, m in [1/2, 1), c = m rounded to 1/256,
+// r = (m - c) / c (|r| <= 2^-8; m - c exact), log x = (e ln2_hi + T_hi) +
+// (r + (r^2 q(r) + (e ln2_lo + T_lo))) with ln c = T_hi + T_lo, T_hi and
+// ln2_hi multiples of 2^-32 so that their sum is exact, q the log1p series
+// to r^8 (truncation < 2^-70 relative).  About 20 VALU and two LDS reads
+// against ~75 VALU for OCML's log; within ~0.5 ulp, so the normals stay
+// within the last ulp of NumPy's (tests/test_gpu_legacy.py).
+__device__ __forceinline__ double log_leg(double x, const double *tab) {
+  const double m = __builtin_amdgcn_frexp_mant(x);
+  const int e = __builtin_amdgcn_frexp_exp(x);
+  const uint32_t ch = ((uint32_t)(__builtin_bit_cast(uint64_t, m) >> 32) + 0x1000u) & 0xFFFFE000u;
+  const uint32_t off = (ch >> 9) & 0xFFFu;   // 16 j
+  const char *tb = reinterpret_cast<const char *>(tab);
+  const double2 t = *reinterpret_cast<const double2 *>(tb + off);
+  const double ic = *reinterpret_cast<const double *>(tb + kLegLogInv * 8 + (off >> 1));
+  const double r = (m - __builtin_bit_cast(double, (uint64_t)ch << 32)) * ic;
+  double q = __builtin_fma(r, -1.0 / 8.0, 1.0 / 7.0);
+  q = __builtin_fma(q, r, -1.0 / 6.0);
+  q = __builtin_fma(q, r, 1.0 / 5.0);
+  q = __builtin_fma(q, r, -1.0 / 4.0);
+  q = __builtin_fma(q, r, 1.0 / 3.0);
+  q = __builtin_fma(q, r, -0.5);
+  const double de = (double)e;
+  const double lo = __builtin_fma(de, 1.90821492927058770002e-10, t.y);
+  const double shi = __builtin_fma(de, 6.93147180369123816490e-01, t.x);   // exact
+  const double p = __builtin_fma(r * r, q, lo);
+  return shi + (r + p);
+}
+
 // s_ord (the windowed kernels): order[j] n per draw j, staged in LDS at the
 // kernel's start.  Read from a.order, every row index was a vector load
 // whose s_waitcnt vmcnt(0) also waited for the step's earlier trace stores
@@ -1055,7 +1089,8 @@ constexpr int kModeAny = -1, kModeGibbs = 0, kModeVardelta = 1, kModeNormal = 2,
 template <class M, int MODE = kModeAny, bool SORD = false>
 __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, M &m,
                                                 double2 *stage = nullptr,
-                                                const uint32_t *s_ord = nullptr) {
+                                                const uint32_t *s_ord = nullptr,
+                                                const double *s_lg = nullptr) {
   constexpr bool kAny = MODE == kModeAny;
   auto ord = [&](int j) -> int64_t {
     if constexpr (SORD) return (int64_t)s_ord[j];
@@ -1183,7 +1218,10 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       auto polar = [&](int k, double &g0, double &g1) {
         const double2 p = stage[k * kBlockLegacy + threadIdx.x];
         const double r2 = p.x * p.x + p.y * p.y;
-        const double f = sqrt(-2.0 * log(r2) / r2);
+        double lr;
+        if constexpr (M::kLogTab) lr = log_leg(r2, s_lg);   // Mt4: the table log
+        else lr = log(r2);
+        const double f = sqrt(-2.0 * lr / r2);
         g0 = f * p.y;
         g1 = f * p.x;
       };
@@ -1274,7 +1312,9 @@ __global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1,
 void legacy_gen_k4_kernel(LegacyArgs a) {
   extern __shared__ w4 s_lw[];
   __shared__ uint32_t s_ord[PBH_MAX_DIM];   // order[j] n (a multiple of 16 B)
+  __shared__ double s_lg[kLegLogDoubles];   // log_leg's table (a multiple of 16 B)
   if (!a.gibbs && threadIdx.x < (unsigned)a.d) s_ord[threadIdx.x] = (uint32_t)(a.order[threadIdx.x] * a.n);
+  for (int i = threadIdx.x; i < kLegLogDoubles; i += kBlockLegacy) s_lg[i] = a.lgtab[i];
   __syncthreads();
   const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
   if (c >= a.n) return;
@@ -1284,7 +1324,8 @@ void legacy_gen_k4_kernel(LegacyArgs a) {
   m.n = a.n;
   m.c = c;
   m.init(a.pos[c], s_lw + threadIdx.x);
-  legacy_gen_body<Mt4<H, MODE != kModeVardelta && MODE != kModeAny>, MODE, true>(a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord);
+  legacy_gen_body<Mt4<H, MODE != kModeVardelta && MODE != kModeAny>, MODE, true>(
+      a, c, m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_ord, s_lg);
   a.pos[c] = m.packed();
 }
 
