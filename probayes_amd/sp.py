@@ -34,6 +34,21 @@ from probayes_amd.rv import RF, RV
 MCMC_SAMPLERS = ('metropolis', 'hastings', 'gibbs')   # sp_utils.py:87-91
 
 
+def _registry_kind(fn, slot):
+  """The sampler name of one of the reference registry's own functions
+  (sp_utils.py:19-85: <name>_scores / _thresh / _update, slot 0 / 1 / 2)
+  passed as an object, identified by its module and name; None for any other
+  callable."""
+  name = getattr(fn, '__name__', None)
+  mod = (getattr(fn, '__module__', None) or '').rsplit('.', 1)[-1]
+  if not callable(fn) or mod != 'sp_utils' or not isinstance(name, str):
+    return None
+  kind, _, part = name.partition('_')
+  if kind in MCMC_SAMPLERS and part == ('scores', 'thresh', 'update')[slot]:
+    return kind
+  return None
+
+
 class FlagArray(np.ndarray):
   """Update flags u with the list API the examples use (u.count(True))."""
 
@@ -70,6 +85,8 @@ class SP:
     self._delta = None     # (delta, args, kwds) or an RF
     self._tfun = None
     self._scores = self._thresh = self._update = None
+    self._scores_fn = False    # scores given as the registry's function object
+    self._scores_pscale = None   # ... and the pscale keyword it was given
     self._samplers = self._counter = self._last = None   # sp.py:113-128
 
   # ---- specification (sp.py:57-100, rf.py:91-304, field.py:220-317) -----
@@ -113,21 +130,37 @@ class SP:
     self._tfun = tfun
 
   def set_scores(self, scores=None, *args, **kwds):
-    self._scores = scores
-    if scores in MCMC_SAMPLERS:
-      self._thresh = self._thresh or scores
-      self._update = self._update or scores
-    elif scores is not None:
+    """sp.py:57-67: a registry name also sets thresh and update; any other
+    callable is wrapped as an Expression with the given arguments -- here
+    only the registry's own functions, passed as objects, lower (as their
+    name, without the cascade; the pscale keyword is checked at lowering)."""
+    self._scores_fn, self._scores_pscale = False, None
+    if scores is None or (isinstance(scores, str) and scores in MCMC_SAMPLERS):
+      self._scores = scores
+      if scores is not None:
+        self._thresh = self._thresh or scores
+        self._update = self._update or scores
+      return
+    kind = _registry_kind(scores, 0)
+    if kind is None:
       raise L.NotLowerable('custom scores callables have no kernel')
+    self._scores, self._scores_fn = kind, True
+    self._scores_pscale = kwds.get('pscale')
 
   def set_thresh(self, thresh=None, *args, **kwds):
-    if thresh is not None and thresh not in MCMC_SAMPLERS:
-      raise L.NotLowerable('custom thresh callables have no kernel')
+    if thresh is not None and not (isinstance(thresh, str) and thresh in MCMC_SAMPLERS):
+      kind = _registry_kind(thresh, 1)
+      if kind is None:
+        raise L.NotLowerable('custom thresh callables have no kernel')
+      thresh = kind
     self._thresh = thresh
 
   def set_update(self, update=None, *args, **kwds):
-    if update is not None and update not in MCMC_SAMPLERS:
-      raise L.NotLowerable('custom update callables have no kernel')
+    if update is not None and not (isinstance(update, str) and update in MCMC_SAMPLERS):
+      kind = _registry_kind(update, 2)
+      if kind is None:
+        raise L.NotLowerable('custom update callables have no kernel')
+      update = kind
     self._update = update
 
   # ---- lowering -----------------------------------------------------------
@@ -223,6 +256,22 @@ class SP:
     ok = ('gibbs',) if scores == 'gibbs' else ('metropolis', 'hastings')
     if self._update not in (None,) + ok or self._thresh not in (None,) + ok:
       raise L.NotLowerable('mixed scores/thresh/update samplers')
+    if self._scores_fn:
+      # the function object sets neither thresh nor update (sp.py:57-67)
+      if self._thresh is None or self._update is None:
+        raise L.NotLowerable('scores given as a function set no thresh / '
+                             'update: set_thresh() and set_update() too')
+      # it scores with the pscale it was given: None is 1 (pscales.py:27-28),
+      # i.e. the stored probabilities taken as linear ones
+      if scores != 'gibbs':
+        sp = self._scores_pscale
+        eff = 'log' if sp is not None and is_log(sp) else \
+              'lin' if sp is None or sp == 1 else None
+        if eff != pscale:
+          raise L.NotLowerable(
+              'scores given as a function with pscale={!r} divide the {}-scaled '
+              'probabilities as {} ones (div_prob, pscales.py:219-236): no '
+              'kernel form'.format(sp, pscale, eff or sp))
     prior = None
     if joint and any(rv.vtype is int for rv in rvs):
       raise L.NotLowerable('joint=True priors of int variables (a uniform '

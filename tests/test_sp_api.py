@@ -252,3 +252,55 @@ def test_samplers_are_not_kept_alive_by_the_registry():
   gc.collect()
   assert ref() is None
   assert len(process.get_counter()) == 0 and len(process.get_last()) == 0
+
+
+def _registry_fn(name):
+  """A stand-in with the identity of the reference registry's function
+  (probayes/sp_utils.py:19-85): the façade recognises it by module and name."""
+  def f(*args, **kwds):
+    raise AssertionError('never called: the kernel runs the sampler')
+  f.__name__ = name
+  f.__module__ = 'probayes.sp_utils'
+  return f
+
+
+def _same_spec(a, b):
+  if isinstance(a, dict):
+    return isinstance(b, dict) and a.keys() == b.keys() and \
+        all(_same_spec(a[k], b[k]) for k in a)
+  if isinstance(a, (list, tuple)):
+    return len(a) == len(b) and all(_same_spec(x, y) for x, y in zip(a, b))
+  if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+    return np.array_equal(np.asarray(a), np.asarray(b), equal_nan=True)
+  return a == b or (a != a and b != b)
+
+
+def test_registry_functions_as_objects():
+  """set_scores / set_thresh / set_update with the registry's own functions
+  passed as objects (sp.py:57-100 wraps them as Expressions): they lower as
+  their names when the scores' pscale keyword matches the model's; with
+  pscale=None the reference divides the log-probabilities as linear ones
+  (pscales.py:27-28, 219-236), which has no kernel form; the function object
+  does not set thresh and update, so they must be given; any other callable
+  still has no kernel."""
+  process, args, kwds, keys, g, t = _build('metrohast_norm1d')
+  extra = args[1] if len(args) > 1 else None
+  ref = process.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  process.set_scores(_registry_fn('hastings_scores'), pscale='log')
+  process.set_thresh(_registry_fn('hastings_thresh'))
+  process.set_update(_registry_fn('metropolis_update'))
+  spec = process.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  assert _same_spec(spec, ref)
+  process.set_scores(_registry_fn('hastings_scores'))      # pscale=None
+  with pytest.raises(pb.NotLowerable):
+    process.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  fresh, *_ = _build('metrohast_norm1d')
+  fresh.set_thresh(None)
+  fresh.set_update(None)
+  fresh.set_scores(_registry_fn('hastings_scores'), pscale='log')
+  with pytest.raises(pb.NotLowerable):                     # no thresh / update
+    fresh.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  with pytest.raises(pb.NotLowerable):
+    process.set_scores(lambda opqr: 1.)
+  with pytest.raises(pb.NotLowerable):
+    process.set_thresh(_registry_fn('hastings_scores'))    # the wrong slot
