@@ -353,22 +353,30 @@ __global__ __launch_bounds__(256) void trace_ess_kernel(
 // positive one, found by a block-wide min.  O(T log T) per series instead of
 // O(T x lags): the GMM chains of cfg5 need a few hundred lags.
 // FFT: Stockham autosort, radix 16 (4096 = 16^3, three passes, 256 threads
-// x 16 points in registers, the 16-point DFT as 4 x 4), in place in LDS
-// (rows padded by one entry per 16: fewer bank conflicts on the strided
-// writes).  Twiddles: one sincospi per pass and thread, powers by products.
-// Series s (= k n + c) and s + 1 are adjacent doubles of every record, so a
-// lane reads both with one 16-byte load; workgroups are mapped so that
-// consecutive pairs share an XCD (and its L2) -- the reads of one record row
-// by neighbouring pairs then hit the same L2 lines.
+// x 16 points in registers, the 16-point DFT as 4 x 4).  Between passes the
+// points are exchanged through ONE 32 KiB array of doubles, real parts then
+// imaginary parts (four barriers per exchange instead of two, half the
+// LDS): four workgroups of four waves fit a CU (a 64 KiB complex buffer
+// held it to two, and two waves per SIMD left the fp64 pipe waiting on
+// latency and barriers).  The array is XOR-swizzled within 16-entry rows
+// (fsw): the stride-16 writes of the first pass and the contiguous reads are
+// then conflict-free for ds_write_b64 / ds_read_b64.
+// Twiddles: one sincospi per transform size and thread (the inverse's are
+// conjugates), powers by a depth-4 product tree.  Series s (= k n + c) and
+// s + 1 are adjacent doubles of every record, so a lane reads both with one
+// 16-byte load; workgroups are mapped so that consecutive pairs share an XCD
+// (and its L2) -- the reads of one record row by neighbouring pairs then hit
+// the same L2 lines.
 // ---------------------------------------------------------------------------
 constexpr int kFftN = 4096, kFftT = 256;   // points, threads
 struct cdbl { double re, im; };
-__device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
+__device__ __forceinline__ int fsw(int e) { return e + (e >> 4); }
 __device__ __forceinline__ cdbl cadd(cdbl a, cdbl b) { return {a.re + b.re, a.im + b.im}; }
 __device__ __forceinline__ cdbl csub(cdbl a, cdbl b) { return {a.re - b.re, a.im - b.im}; }
 __device__ __forceinline__ cdbl cmul(cdbl a, cdbl b) {
   return {__builtin_fma(a.re, b.re, -(a.im * b.im)), __builtin_fma(a.re, b.im, a.im * b.re)};
 }
+__device__ __forceinline__ cdbl conj(cdbl a) { return {a.re, -a.im}; }
 // times SIGN i
 template <int SIGN>
 __device__ __forceinline__ cdbl cmuli(cdbl a) {
@@ -405,40 +413,64 @@ __device__ __forceinline__ void dft16(cdbl (&v)[16]) {
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) dft4<SIGN>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
 }
-// One Stockham pass (sub-transform size NS -> 16 NS), in place: all loads,
-// barrier, all stores, barrier.
-template <int SIGN, int NS>
-__device__ __forceinline__ void fft_pass(cdbl *buf) {
-  const int j = (int)threadIdx.x;
-  cdbl v[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = buf[fpad(j + r * kFftT)];
+// The arithmetic of one Stockham pass (sub-transform size NS -> 16 NS) on
+// the thread's points v[r] = x[j + 256 r]: twiddle, 16-point DFT.  w = exp(SIGN
+// 2 pi i m / (16 NS)), m = j % NS.  IN_HALF:
+// v[8..15] are zero (the padded series) and are not multiplied.
+template <int SIGN, int NS, bool IN_HALF = false>
+__device__ __forceinline__ void fft_compute(cdbl (&v)[16], cdbl w) {
   if constexpr (NS > 1) {
-    const int m = j % NS;
-    double sn, cs;
-    sincospi((double)(SIGN * 2 * m) / (double)(16 * NS), &sn, &cs);
-    const cdbl w{cs, sn};
-    cdbl wr = w;
+    // w^(4 a + b) = w^(4 a) w^b: six powers live, each other one formed
+    // just before its product (14 complex products in all)
+    const cdbl p1 = w, p2 = cmul(w, w), p3 = cmul(p2, w), p4 = cmul(p2, p2);
+    const cdbl p8 = cmul(p4, p4), p12 = cmul(p8, p4);
+    const cdbl pb[4] = {cdbl{1., 0.}, p1, p2, p3}, pa[4] = {cdbl{1., 0.}, p4, p8, p12};
 #pragma unroll
     for (int r = 1; r < 16; ++r) {
-      v[r] = cmul(v[r], wr);
-      if (r < 15) wr = cmul(wr, w);
+      if (IN_HALF && r >= 8) continue;
+      const int a = r >> 2, b = r & 3;
+      v[r] = cmul(v[r], a == 0 ? pb[b] : b == 0 ? pa[a] : cmul(pa[a], pb[b]));
     }
   }
   dft16<SIGN>(v);
+}
+// where a pass leaves output v[i] (i = 4 k1 + k2): base + (k1 + 4 k2) NS
+template <int NS>
+__device__ __forceinline__ int fft_out(int i) {
+  const int j = (int)threadIdx.x;
+  return (j / NS) * NS * 16 + (j % NS) + ((i >> 2) + 4 * (i & 3)) * NS;
+}
+// Move the pass outputs (fft_out<NS>) to the next pass's inputs
+// (x[j + 256 r] in v[r]) through sb, real parts then imaginary parts.
+template <int NS>
+__device__ __forceinline__ void fft_exchange(double *sb, cdbl (&v)[16]) {
+  const int j = (int)threadIdx.x;
+  double t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<NS>(i))] = v[i].re;
   __syncthreads();
-  const int base = (j / NS) * NS * 16 + (j % NS);
 #pragma unroll
-  for (int k1 = 0; k1 < 4; ++k1)
+  for (int r = 0; r < 16; ++r) t[r] = sb[fsw(j + r * kFftT)];
+  __syncthreads();
 #pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2) buf[fpad(base + (k1 + 4 * k2) * NS)] = v[4 * k1 + k2];
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<NS>(i))] = v[i].im;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = cdbl{t[r], sb[fsw(j + r * kFftT)]};
   __syncthreads();
 }
-template <int SIGN>
-__device__ __forceinline__ void fft4096(cdbl *buf) {
-  fft_pass<SIGN, 1>(buf);
-  fft_pass<SIGN, 16>(buf);
-  fft_pass<SIGN, 256>(buf);
+// the twiddle bases of passes 2 and 3 (NS = 16, 256) for SIGN = -1; the
+// inverse transform's are their conjugates
+struct FftTw { cdbl w16, w256; };
+__device__ __forceinline__ FftTw fft_twiddles() {
+  const int j = (int)threadIdx.x;
+  FftTw t;
+  double sn, cs;
+  sincospi(-(double)(2 * (j % 16)) / 256.0, &sn, &cs);
+  t.w16 = cdbl{cs, sn};
+  sincospi(-(double)(2 * (j % 256)) / 4096.0, &sn, &cs);
+  t.w256 = cdbl{cs, sn};
+  return t;
 }
 
 // block-wide sum / min over the 256 threads (red: 8 scratch entries)
@@ -461,9 +493,10 @@ __device__ __forceinline__ int block_min(int v, int *red) {
   return min(min(red[0], red[1]), min(red[2], red[3]));
 }
 
-__global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
-    const double *tx, int64_t n, int32_t d, int64_t first, int32_t T, double *ess) {
-  __shared__ cdbl buf[kFftN + kFftN / 16];
+__global__ __launch_bounds__(kFftT) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void trace_ess_fft_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
+                          int32_t T, double *ess) {
+  __shared__ double sb[kFftN + kFftN / 16];
   __shared__ double red[8];
   __shared__ int ired[8];
   // XCD-aware pair index: block b runs on XCD b % 8; give each XCD a
@@ -479,7 +512,7 @@ __global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
   const double *src = tx + first * row + s0;
   // ---- load (t = j + 256 q, q < 8: T <= 2048) and centre ----
   double xa[8], xb[8];
-  double sa = 0., sb = 0.;
+  double sa = 0., sb_ = 0.;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int t = j + q * kFftT;
@@ -500,36 +533,67 @@ __global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
       }
     }
     sa += xa[q];
-    sb += xb[q];
+    sb_ += xb[q];
   }
   const double ma = block_sum(sa, red) / (double)T;
-  const double mb = block_sum(sb, red + 4) / (double)T;
+  const double mb = block_sum(sb_, red + 4) / (double)T;
+  const FftTw tw = fft_twiddles();
+  // ---- forward transform of a + i b (points 2048 .. 4095 zero): the
+  // thread's points x[j + 256 r] are already in registers ----
+  cdbl v[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int t = j + q * kFftT;
-    cdbl z{0., 0.};
-    if (q < 8 && t < T) z = cdbl{xa[q] - ma, has_b ? xb[q] - mb : 0.};
-    buf[fpad(t)] = z;
+    v[q] = cdbl{0., 0.};
+    if (q < 8 && t < T) v[q] = cdbl{xa[q] - ma, has_b ? xb[q] - mb : 0.};
   }
+  fft_compute<-1, 1, true>(v, cdbl{1., 0.});
+  fft_exchange<1>(sb, v);
+  fft_compute<-1, 16>(v, tw.w16);
+  fft_exchange<16>(sb, v);
+  fft_compute<-1, 256>(v, tw.w256);
+  // ---- unpack the two spectra (Z_k and Z_{N-k}), pack |X|^2 + i |Y|^2 at
+  // k = j + 256 q: the inverse transform's first-pass points ----
+  double xr[16], yi[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<256>(i))] = v[i].re;
   __syncthreads();
-  fft4096<-1>(buf);
-  // ---- unpack the two spectra, pack |X|^2 + i |Y|^2 ----
-  cdbl pk[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int k = j + q * kFftT;
-    const cdbl zk = buf[fpad(k)], zm = buf[fpad((kFftN - k) & (kFftN - 1))];
-    const double xr = zk.re + zm.re, xi = zk.im - zm.im;   // 2 X_k
-    const double yr = zk.im + zm.im, yi = zm.re - zk.re;   // 2 Y_k
-    pk[q] = cdbl{__builtin_fma(xr, xr, xi * xi), __builtin_fma(yr, yr, yi * yi)};
+    const double zk = sb[fsw(k)], zm = sb[fsw((kFftN - k) & (kFftN - 1))];
+    xr[q] = zk + zm;   // 2 Re X_k
+    yi[q] = zm - zk;   // 2 Im Y_k
   }
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) buf[fpad(j + q * kFftT)] = pk[q];
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<256>(i))] = v[i].im;
   __syncthreads();
-  fft4096<1>(buf);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = j + q * kFftT;
+    const double zk = sb[fsw(k)], zm = sb[fsw((kFftN - k) & (kFftN - 1))];
+    const double xi = zk - zm, yr = zk + zm;   // 2 Im X_k, 2 Re Y_k
+    v[q] = cdbl{__builtin_fma(xr[q], xr[q], xi * xi), __builtin_fma(yr, yr, yi[q] * yi[q])};
+  }
+  __syncthreads();
+  // ---- inverse transform; only lags 0 .. 2047 are kept ----
+  fft_compute<1, 1>(v, cdbl{1., 0.});
+  fft_exchange<1>(sb, v);
+  fft_compute<1, 16>(v, conj(tw.w16));
+  fft_exchange<16>(sb, v);
+  fft_compute<1, 256>(v, conj(tw.w256));
+  // autocovariances of a in sb[0, 2048), of b in sb[2048, 4096)
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((i & 3) < 2) {   // lag fft_out<256>(i) < 2048
+      const int e = fsw(fft_out<256>(i));
+      sb[e] = v[i].re;
+      sb[kFftN / 2 + kFftN / 32 + e] = v[i].im;
+    }
+  __syncthreads();
   // ---- Geyer's initial positive sequence on both series ----
-  const double a0 = buf[0].re, b0 = buf[0].im;
+  const double a0 = sb[0], b0 = sb[kFftN / 2 + kFftN / 32];
   const double ia = 1.0 / (a0 > 1e-300 ? a0 : 1e-300);
   const double ib = 1.0 / (b0 > 1e-300 ? b0 : 1e-300);
   const int m = (T - 1) / 2;   // pairs (lags 2J + 1, 2J + 2), J < m
@@ -540,9 +604,9 @@ __global__ __launch_bounds__(kFftT) void trace_ess_fft_kernel(
     const int J = j + q * kFftT;
     pa[q] = pb[q] = 0.;
     if (J < m) {
-      const cdbl u = buf[fpad(2 * J + 1)], v = buf[fpad(2 * J + 2)];
-      pa[q] = u.re * ia + v.re * ia;
-      pb[q] = u.im * ib + v.im * ib;
+      const int e1 = fsw(2 * J + 1), e2 = fsw(2 * J + 2);
+      pa[q] = sb[e1] * ia + sb[e2] * ia;
+      pb[q] = sb[kFftN / 2 + kFftN / 32 + e1] * ib + sb[kFftN / 2 + kFftN / 32 + e2] * ib;
       if (pa[q] <= 0. && J < fa) fa = J;
       if (pb[q] <= 0. && J < fb) fb = J;
     }
