@@ -819,8 +819,13 @@ struct Mt4 {
     }
     if (__builtin_amdgcn_ballot_w64(hq - aq() <= H)) {
       if (hq - aq() <= H) {
-        if (!pf) prefetch();   // not loaded ahead (its block was not twisted then)
-        commit();
+        // loaded ahead (complete since the last step's mid-step wait), or not
+        // (its block was not twisted then): the same chunks staged out of
+        // line, so that the common path's code carries no wait for loads
+        // just issued (one shared commit waited vmcnt down to 0 -- i.e. for
+        // the last step's trace stores -- on both paths)
+        if (pf) commit();
+        else refill_cold();
       }
     }
     // the next refill, ahead (whenever its blocks are twisted)
@@ -1098,6 +1103,11 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
   };
   double gauss = a.gauss[c];
   int has = a.has_gauss[c];
+  // every load before the step loop completes here, once: a load result
+  // carried into the loop (gauss, has) otherwise made the wait pass put an
+  // s_waitcnt vmcnt(0) at its first use in EVERY step -- which also waited
+  // for the previous step's trace stores and the prefetch just issued
+  __builtin_amdgcn_s_waitcnt(0);
   const int64_t rowlen = (int64_t)a.R * a.n;
   for (int64_t t = 0; t < a.n_steps; ++t) {
     double *row = a.out + t * rowlen + c;
@@ -1209,6 +1219,13 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
           }
         }
       }
+      // Wait here for this step's window prefetch (issued at the step top,
+      // complete by now) and the previous step's trace stores (issued ~a step
+      // ago): vmcnt(0) only, once per step, before this step's stores.  The
+      // prefetched chunks are then complete in the compiler's view, so the
+      // commit that consumes them in a later step needs no vmcnt(0) -- which
+      // there also waited for the round trip of the stores just issued.
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt / lgkmcnt untouched
       // the pairs' transcendental part, two independent pairs per
       // iteration (one basic block: the scheduler interleaves their log /
       // division / square-root chains); a last pair whose second deviate is
