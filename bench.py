@@ -297,6 +297,10 @@ def main():
     cpu = cpu_baseline()
 
   sha = lib_sha256()   # the binary the line (and its traffic profile) is of
+  # this process is the host application and owns the device: spin-wait on
+  # completion signals (hipDeviceScheduleSpin, process-wide, opt-in at
+  # pbh_create; a short launch is seen to end ~2 us sooner)
+  os.environ.setdefault('PBH_SPIN_FLAG', '1')
   from probayes_amd import Engine
   eng = Engine(cfg2_spec(), device=local)
   col = None

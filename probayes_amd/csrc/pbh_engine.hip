@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <algorithm>
 #include <chrono>
 #include <vector>
 
@@ -88,13 +89,11 @@ struct pbh_engine {
                              // (512: one table copy per CU, 20-step launches ~5 % faster)
   // Launches of <= 64 steps (the driver's 20-step shape): the alternation
   // clock starts at each wave's loop entry and hands over once, half-way
-  // (2^10 ticks = 10.24 us for 20 steps), shifted by fair_off ticks -- the
+  // (2^10 ticks = 10.24 us for 20 steps) -- the
   // free-running clock put the one hand-over anywhere in the launch or nowhere
   // (profiles/r04f_phase.jsonl: the last wave ends 26.4-29.2 us into a k11
   // launch, 26.5-26.6 us with the launch-relative clock)
   int fair_short = 10;       // PBH_FAIR_SHORT=k
-  int fair_off = 0;          // PBH_FAIR_OFF=ticks
-  int bal = 0;               // PBH_BAL=D: progress-balanced wave priorities (512 WG)
   int fair_rel = 0;          // PBH_FAIR_REL=1: long launches use the relative clock too
   bool event_markers = true;
   bool pair_enabled = true;  // PBH_NO_PAIR=1 disables the lane-pair kernel
@@ -219,12 +218,18 @@ int pbh_create(int device, pbh_engine **out) {
   // The runtime spins on completion signals instead of yielding / sleeping
   // on them (hipDeviceScheduleSpin): the host sees a short launch end ~2 us
   // sooner (tools/ubench/launch_lat.hip, profiles/r04d_launch_lat.jsonl).
-  // Process-wide for the device; a device already in use keeps its flags
-  // (the call then fails, harmlessly).  PBH_SPIN_FLAG=0 leaves the default.
+  // The flag is process-wide for the device, so it is the host
+  // application's choice: opt-in with PBH_SPIN_FLAG=1 (bench.py sets it).  A
+  // device already in use keeps its flags (the call then fails, harmlessly);
+  // only that call's own error is cleared, never one the application had
+  // pending before it.
   {
     const char *sf = std::getenv("PBH_SPIN_FLAG");
-    if (!sf || sf[0] != '0') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
-    (void)hipGetLastError();
+    if (sf && sf[0] == '1') {
+      const hipError_t before = hipPeekAtLastError();
+      if (hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess && before == hipSuccess)
+        (void)hipGetLastError();
+    }
   }
   pbh_engine *e = new pbh_engine();
   e->device = device;
@@ -247,9 +252,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *wg = std::getenv("PBH_PAIR_WG")) e->pair_wg = std::atoi(wg);
   if (const char *fs = std::getenv("PBH_FAIR_SHORT"))
     e->fair_short = std::min(20, std::max(0, std::atoi(fs)));
-  if (const char *b = std::getenv("PBH_BAL")) e->bal = std::min(64, std::max(0, std::atoi(b)));
   if (const char *fr = std::getenv("PBH_FAIR_REL")) e->fair_rel = std::atoi(fr) != 0;
-  if (const char *fo = std::getenv("PBH_FAIR_OFF")) e->fair_off = std::atoi(fo);
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   if (const char *lk = std::getenv("PBH_LEGACY_K4")) e->legacy_k4 = std::atoi(lk) != 0;
@@ -810,7 +813,23 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
     HIP_TRY(hipMemcpy(e->lgtab, lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
   }
   a.lgtab = e->lgtab;
-  hipError_t err = pbh::launch_legacy_gen(a, e->stream);
+  // Launches of at most kLegacyLaunchSteps steps: the generator counts a
+  // launch's stream quads per chain in 32-bit ints (Mt4's head index), and a
+  // step takes a bounded-in-expectation but unbounded number of words (polar
+  // rejections, randint masks), so the launch length is what is bounded:
+  // 2^20 steps x R <= 33 draws x ~3 words per draw is ~2^27 quads << 2^31.
+  // The state (position, block, pending gauss) persists between launches, so
+  // the split is invisible in the stream.
+  constexpr int64_t kLegacyLaunchSteps = int64_t(1) << 20;
+  hipError_t err = hipSuccess;
+  for (int64_t done = 0; done < n_steps && err == hipSuccess;) {
+    const int64_t k = std::min(n_steps - done, kLegacyLaunchSteps);
+    a.out = e->rep + (size_t)done * R * n;
+    a.n_steps = k;
+    a.step0 = e->g + done;
+    err = pbh::launch_legacy_gen(a, e->stream);
+    done += k;
+  }
   if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
   if (err != hipSuccess)
     return fail(PBH_ERR_HIP, "pbh_legacy_replay: %s", hipGetErrorString(err));
@@ -1010,8 +1029,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.iid_full = e->iid_full ? 1 : 0;
   k.iid_pair = e->iid_pair ? 1 : 0;
   k.fair = e->fair;
-  k.pair_wg = e->bal ? 512 : e->pair_wg;
-  k.bal = e->bal;
+  k.pair_wg = e->pair_wg;
   k.gq = e->gq;
   const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;
@@ -1040,7 +1058,6 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     const bool short_launch = m <= 64;
     k.fair = short_launch ? e->fair_short : e->fair;
     k.fair_rel = short_launch ? 1 : e->fair_rel;
-    k.fair_off = short_launch ? e->fair_off : 0;
     k.g0 = e->g;
     k.has_pred = e->has_pred ? 1 : 0;
     k.rep_row0 = e->g - e->rep_g0;

@@ -124,8 +124,6 @@ struct KArgs {
   int32_t fair;        // alternate the SIMD's wave priorities every 2^fair real-time ticks (0: off)
   int32_t pair_wg;     // FULL pair kernel's workgroup size (256 or 512)
   int32_t fair_rel;    // FULL pair kernel: the alternation clock starts at the wave's loop entry
-  int32_t fair_off;    // with fair_rel: the first hand-over comes fair_off ticks later
-  int32_t bal;         // FULL pair kernel (512 WG): the SIMD's two waves trade priority by progress, gap D pairs (0: off)
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;

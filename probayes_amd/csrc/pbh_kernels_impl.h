@@ -1369,14 +1369,6 @@ void mh_pair_kernel(KArgs a) {
   Xo xs{0u, 0u, 0u, 0u};
   if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, h, cc);
 
-  // FULL with a.bal: the SIMD's two waves (one 512-thread workgroup) post
-  // their progress in LDS; the slot counters are zeroed before the table
-  // load's barrier
-  __shared__ uint32_t s_prog[8], s_cnt[4];
-  if (FULL && threadIdx.x < 8) {
-    s_prog[threadIdx.x] = 0u;
-    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0u;
-  }
   // the LDS tables after the state's loads: all of them in flight at once
   if constexpr (FULL) bm64_commit(s_bmt, tabr);
   else if constexpr (TAB) bm64_load(s_bmt, a.bm64);
@@ -1695,41 +1687,14 @@ void mh_pair_kernel(KArgs a) {
           if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // no stores in flight yet
           PBH_PHASE(2);
           const uint32_t slot = a.fair ? simd_wave_slot() : 0u;
-          // a.bal: this wave's and its SIMD partner's progress slots
-          uint32_t me = 0u, partner = 0u;
-          if (a.bal) {
-            const uint32_t simd = simd_id();
-            uint32_t idx = 0u;
-            if (lane == 0) idx = __hip_atomic_fetch_add(&s_cnt[simd], 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            idx = __builtin_amdgcn_readfirstlane(idx) & 1u;
-            me = 2u * simd + idx;
-            partner = me ^ 1u;
-            PBH_PHASE_TAG(me + 1u);
-          }
-          uint32_t other = 0u;   // the partner's progress read one pair ago
           // a.fair_rel: the alternation's clock starts at this wave's loop
           // entry (the waves of a launch start within ~0.4 us of each other),
           // so the hand-overs of a short launch fall at the same points of
           // every launch instead of wherever the free-running clock is
           const uint64_t tfair0 =
-              a.fair_rel ? __builtin_amdgcn_s_memrealtime() + (int64_t)a.fair_off : 0ull;
+              a.fair_rel ? __builtin_amdgcn_s_memrealtime() : 0ull;
           for (; s + 3 < a.n_steps; s += 2) {
-            if (a.bal) {
-              // the wave that is more than a.bal pairs behind its partner
-              // takes the lead (priority 1) until it is a.bal pairs ahead:
-              // a leader / filler interleave whose roles trade, so both waves
-              // end together instead of the younger one finishing alone
-              const int mine = s >> 1;
-              const int gap = (int)__builtin_amdgcn_readfirstlane(other) - mine;
-              if (gap > a.bal) __builtin_amdgcn_s_setprio(1);
-              else if (gap < -a.bal) __builtin_amdgcn_s_setprio(0);
-              if (lane == 0)
-                __hip_atomic_store(&s_prog[me], (uint32_t)mine, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-              other = __hip_atomic_load(&s_prog[partner], __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if (a.fair) {
+            if (a.fair) {
               const int64_t el = (int64_t)(__builtin_amdgcn_s_memrealtime() - tfair0);
               fair_prio((uint32_t)((el > 0 ? (uint64_t)el : 0ull) >> a.fair) + slot);
             }

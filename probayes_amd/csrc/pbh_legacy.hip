@@ -712,9 +712,10 @@ __device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win,
 }
 // the rare refills (a launch's first, a step longer than the window) out of
 // line; the head's block is twisted first if nothing has (values in and out:
-// returns hq | ready << 24)
+// returns (ready << 32) | hq, each a full 32-bit field: hq counts the launch's
+// quads per chain and grows past 2^24 in a launch of a few million steps)
 template <int H, bool DBL>
-__device__ __attribute__((noinline)) int mt4_refill_cold(w4 *key, int64_t n, int64_t c,
+__device__ __attribute__((noinline)) uint64_t mt4_refill_cold(w4 *key, int64_t n, int64_t c,
                                                          w4 *win, int hq, int blk, int cb,
                                                          int ready) {
 #pragma unroll 1
@@ -726,7 +727,7 @@ __device__ __attribute__((noinline)) int mt4_refill_cold(w4 *key, int64_t n, int
     }
     hq += mt4_stage<DBL>(key, n, c, win, 2 * H, (cb + hb - blk) & 3, hc, hq);
   }
-  return hq | (ready << 24);
+  return ((uint64_t)(uint32_t)ready << 32) | (uint32_t)hq;
 }
 
 template <int H, bool DBL = false>
@@ -757,9 +758,9 @@ struct Mt4 {
   __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
 
   __device__ __forceinline__ void refill_cold() {
-    const int r = mt4_refill_cold<H, DBL>(key, n, c, win, hq, blk, cb, ready);
-    hq = r & 0xFFFFFF;
-    ready = r >> 24;
+    const uint64_t r = mt4_refill_cold<H, DBL>(key, n, c, win, hq, blk, cb, ready);
+    hq = (int)(uint32_t)r;
+    ready = (int)(uint32_t)(r >> 32);
     hb = hq / kQ;
     hc = (hq - hb * kQ) >> 3;
     pf = false;   // the head moved: a prefetched refill is stale

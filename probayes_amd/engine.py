@@ -345,12 +345,22 @@ class Engine:
       _lib.call('pbh_legacy_state_words', self._h, _c.byref(words))
       want = {'key': (words.value, self.n), 'pos': (self.n,), 'has': (self.n,),
               'gauss': (self.n,)}
+      layouts = {2560: 'Mt4, four chunked blocks (the default)',
+                 1248: 'double-buffered window (PBH_LEGACY_K4=0, round 3)',
+                 624: 'in-place state (PBH_LEGACY_DB=0, round 1)'}
       for k, shape in want.items():
         got = np.shape(mt[k])
         if got != shape:
+          hint = ''
+          if k == 'key' and len(got) == 2 and got[1] == self.n:
+            hint = ('; the checkpoint holds the {} layout, this engine the {}: '
+                    'restore it in an engine created with that layout\'s '
+                    'environment'.format(
+                        layouts.get(got[0], '{}-word'.format(got[0])),
+                        layouts.get(words.value, '{}-word'.format(words.value))))
           raise ValueError('checkpoint legacy state {} has shape {}, this engine '
-                           'needs {} (legacy layout words per chain: {})'.format(
-                               k, got, shape, words.value))
+                           'needs {} (legacy layout words per chain: {}){}'.format(
+                               k, got, shape, words.value, hint))
     _lib.call('pbh_restore', self._h, _dp(x), _dp(lp),
               _c.c_int64(int(ck['step'])), 1 if ck['has_pred'] else 0,
               None if xo is None else xo.ctypes.data_as(_lib._u32p))

@@ -37,16 +37,23 @@ MCMC_SAMPLERS = ('metropolis', 'hastings', 'gibbs')   # sp_utils.py:87-91
 def _registry_kind(fn, slot):
   """The sampler name of one of the reference registry's own functions
   (sp_utils.py:19-85: <name>_scores / _thresh / _update, slot 0 / 1 / 2)
-  passed as an object, identified by its module and name; None for any other
-  callable."""
+  passed as an object, identified by its module (exactly probayes.sp_utils:
+  a user's own module of that name holds other semantics) and name; None for
+  any other callable."""
   name = getattr(fn, '__name__', None)
-  mod = (getattr(fn, '__module__', None) or '').rsplit('.', 1)[-1]
-  if not callable(fn) or mod != 'sp_utils' or not isinstance(name, str):
+  mod = getattr(fn, '__module__', None)
+  if not callable(fn) or mod != 'probayes.sp_utils' or not isinstance(name, str):
     return None
   kind, _, part = name.partition('_')
   if kind in MCMC_SAMPLERS and part == ('scores', 'thresh', 'update')[slot]:
     return kind
   return None
+
+
+def _no_spec_args(name, args, kwds):
+  """sp.py:62-63, 79-80, 96-97: a registry name takes no arguments."""
+  assert not args and not kwds, \
+      "Neither args nor kwds permitted with spec '{}'".format(name)
 
 
 class FlagArray(np.ndarray):
@@ -130,38 +137,69 @@ class SP:
     self._tfun = tfun
 
   def set_scores(self, scores=None, *args, **kwds):
-    """sp.py:57-67: a registry name also sets thresh and update; any other
-    callable is wrapped as an Expression with the given arguments -- here
-    only the registry's own functions, passed as objects, lower (as their
-    name, without the cascade; the pscale keyword is checked at lowering)."""
+    """sp.py:57-67: a registry name sets the scores and, through set_thresh,
+    thresh and update too, overwriting any earlier ones (sp.py:64-65, 81-82);
+    None clears the scores only.  Any other callable is wrapped as an
+    Expression with the given arguments -- here only the registry's own
+    scores functions, passed as objects, lower (as their name, without the
+    cascade), with pscale given as a keyword (checked at lowering); other
+    arguments change what the function computes and raise NotLowerable."""
     self._scores_fn, self._scores_pscale = False, None
-    if scores is None or (isinstance(scores, str) and scores in MCMC_SAMPLERS):
+    if scores is None:
+      self._scores = None
+      return
+    if isinstance(scores, str) and scores in MCMC_SAMPLERS:
+      _no_spec_args(scores, args, kwds)
       self._scores = scores
-      if scores is not None:
-        self._thresh = self._thresh or scores
-        self._update = self._update or scores
+      self.set_thresh(scores)
       return
     kind = _registry_kind(scores, 0)
     if kind is None:
       raise L.NotLowerable('custom scores callables have no kernel')
+    if kind != 'gibbs' and (args or set(kwds) - {'pscale'}):
+      raise L.NotLowerable(
+          '{}_scores with arguments {!r} {!r}: only the pscale keyword has a '
+          'kernel form'.format(kind, args, kwds))
     self._scores, self._scores_fn = kind, True
     self._scores_pscale = kwds.get('pscale')
 
   def set_thresh(self, thresh=None, *args, **kwds):
-    if thresh is not None and not (isinstance(thresh, str) and thresh in MCMC_SAMPLERS):
-      kind = _registry_kind(thresh, 1)
-      if kind is None:
-        raise L.NotLowerable('custom thresh callables have no kernel')
-      thresh = kind
-    self._thresh = thresh
+    """sp.py:74-84: a registry name also sets update (overwriting it)."""
+    if thresh is None:
+      self._thresh = None
+      return
+    if isinstance(thresh, str) and thresh in MCMC_SAMPLERS:
+      _no_spec_args(thresh, args, kwds)
+      self._thresh = thresh
+      self.set_update(thresh)
+      return
+    kind = _registry_kind(thresh, 1)
+    if kind is None:
+      raise L.NotLowerable('custom thresh callables have no kernel')
+    if kind != 'gibbs' and (args or kwds):
+      # metropolis_thresh(*args) is np.random.uniform(*args): other limits
+      raise L.NotLowerable(
+          '{}_thresh with arguments {!r} {!r} draws np.random.uniform({}) '
+          '(sp_utils.py:30-31): the kernels draw U(0, 1)'.format(
+              kind, args, kwds, ', '.join(map(repr, args))))
+    self._thresh = kind
 
   def set_update(self, update=None, *args, **kwds):
-    if update is not None and not (isinstance(update, str) and update in MCMC_SAMPLERS):
-      kind = _registry_kind(update, 2)
-      if kind is None:
-        raise L.NotLowerable('custom update callables have no kernel')
-      update = kind
-    self._update = update
+    """sp.py:91-100."""
+    if update is None:
+      self._update = None
+      return
+    if isinstance(update, str) and update in MCMC_SAMPLERS:
+      _no_spec_args(update, args, kwds)
+      self._update = update
+      return
+    kind = _registry_kind(update, 2)
+    if kind is None:
+      raise L.NotLowerable('custom update callables have no kernel')
+    if kind != 'gibbs' and (args or kwds):
+      raise L.NotLowerable('{}_update takes no arguments (sp_utils.py:34-37)'
+                           .format(kind))
+    self._update = kind
 
   # ---- lowering -----------------------------------------------------------
   def _pscale(self, kw_pscale):

@@ -276,3 +276,89 @@ def test_failure_vote_survives_a_nan_dropping_max():
   fill = np.frombuffer(bytes([0x3F]) * 8, np.float64)[0]
   assert np.isfinite(fill) and 0. < fill < 1.
   assert 'a rank could not take part' in vote_message('x', fill)
+
+
+MAIN_WORKER = ENGINE_STANDIN + r'''
+import functools, io, json, contextlib
+import bench
+import probayes_amd
+from probayes_amd.dist import TcpCollective
+from probayes_amd.engine import unpack_stats
+rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+
+
+class MainEngine(OracleEngine):
+  """The Engine interface bench.main() uses, RCCL calls included: the uid
+  is 128 bytes as pbh_rccl_unique_id's, the collectives go over the stdlib
+  TCP stand-in (its own port, next to the uid hand-off's)."""
+  def __init__(self, spec, device=0):
+    OracleEngine.__init__(self, spec)
+    self.device = device
+  @staticmethod
+  def rccl_unique_id():
+    return bytes(range(128))
+  def rccl_init(self, rank_, world_, uid):
+    assert uid == bytes(range(128)) and self.device == rank_
+    self.col = TcpCollective(rank_, world_, '127.0.0.1',
+                             int(os.environ['MASTER_PORT']) + 2)
+  def rccl_allreduce_max(self, v):
+    return self.col.allreduce_max(v)
+  def rccl_allgather_stats(self):
+    s, q, a = self.stats
+    blk, counts = self.col.allgather_stats(s, q, a)
+    return unpack_stats(blk, counts, bench.D)
+  def close(self):
+    self.col.close()
+
+
+probayes_amd.Engine = MainEngine        # main() imports it from the package
+bench.lib_sha256 = lambda: 'standin'    # no library file needed on CPU
+bench.cpu_baseline = functools.partial(bench.cpu_baseline, budget_s=0.3,
+                                       chains=256)
+sys.argv = ['bench.py', '--gpus', str(world), '--steps', '12', '--warmup',
+            '5', '--chains', '6', '--steps-per-launch', '4']
+buf = io.StringIO()
+with contextlib.redirect_stdout(buf):
+  bench.main()
+out = buf.getvalue()
+if rank == 0:
+  lines = [l for l in out.splitlines() if l.strip()]
+  assert len(lines) == 1, out
+  line = json.loads(lines[0])
+  assert line['n_gpus'] == world and line['steps'] == 12, line
+  el = line['ms_per_step'] * 12 / 1e3            # the max over ranks
+  assert abs(line['value'] * el / (6 * world * 12) - 1) < 1e-9, line
+  assert line['cpu_baseline']['cores'] >= 1 and line['cpu_baseline']['value'] > 0
+  assert line['rccl_allgather_ms'] >= 0
+  assert line['roofline']['bound'] == 'hbm' and line['roofline']['frac'] > 0
+  assert line['config']['parallelism'] == 'chain-sharded x{{}}'.format(world)
+  assert line['scaling'] == 'weak'
+  print('MAIN_OK')
+else:
+  assert out == '', out
+  print('QUIET_OK')
+'''
+
+
+def test_two_rank_bench_main_prints_one_scale_line(tmp_path):
+  """VERDICT r04 item 7: bench.main() itself at world 2 -- the CPU baseline
+  on rank 0 before the uid hand-off, the --gpus / WORLD_SIZE check, the
+  RCCL barrier / max / all-gather calls (swapped for the TCP stand-in), the
+  SCALE line's fields -- with exactly one line from rank 0 and nothing from
+  the other rank, both exiting 0."""
+  script = tmp_path / 'main.py'
+  script.write_text(MAIN_WORKER.format(root=ROOT))
+  outs = _spawn(script, 2, _free_port())
+  assert 'MAIN_OK' in outs[0] and 'QUIET_OK' in outs[1], outs
+
+
+def test_bench_main_rejects_a_world_size_mismatch(tmp_path):
+  script = tmp_path / 'mismatch.py'
+  script.write_text('import sys\nsys.path.insert(0, {root!r})\nimport bench\n'
+                    'sys.argv = ["bench.py", "--gpus", "2"]\nbench.main()\n'
+                    .format(root=ROOT))
+  env = dict(os.environ, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+  p = subprocess.run([sys.executable, str(script)], env=env, text=True,
+                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                     timeout=120)
+  assert p.returncode != 0 and 'WORLD_SIZE 1' in p.stdout, p.stdout

@@ -487,9 +487,10 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
 @pytest.mark.parametrize('n', [4096 + 5, 37])
 def test_iid_steady_state_form_is_the_general_form(monkeypatch, pair, n):
   """cfg1's steady-state launch (iid-Normal target, spherical delta, ufun on
-  sigma, uniform prior, e-tempered ratio form) -- on lane pairs
-  (mh_iid_pair_kernel, PBH_IID_PAIR=1, the default) or one lane per chain
-  (mh_iid_full_kernel) -- is bit-for-bit mh_kernel's general form
+  sigma, uniform prior, e-tempered ratio form) -- on one lane per chain
+  (mh_iid_full_kernel, the default, PBH_IID_PAIR=0) or on lane pairs
+  (mh_iid_pair_kernel, opt-in PBH_IID_PAIR=1, measured slower) -- is
+  bit-for-bit mh_kernel's general form
   (PBH_IID_FULL=0): ragged chain counts (padding lanes write nothing; an odd
   number of 32-chain wavefronts leaves the last accept word half-owned),
   launches of 1 and 13 steps starting on either step of a pair, chains

@@ -304,3 +304,53 @@ def test_registry_functions_as_objects():
     process.set_scores(lambda opqr: 1.)
   with pytest.raises(pb.NotLowerable):
     process.set_thresh(_registry_fn('hastings_scores'))    # the wrong slot
+
+
+def test_registry_name_cascade_overwrites():
+  """sp.py:57-66, 74-83: set_scores(name) overwrites thresh and update
+  (through set_thresh), set_thresh(name) overwrites update; a registry name
+  with arguments is an AssertionError; set_scores(None) clears the scores
+  only."""
+  process, args, kwds, keys, g, t = _build('metrohast_norm1d')
+  extra = args[1] if len(args) > 1 else None
+  lw = lambda p: p.lower(extra, kwds.get('iid', False), kwds.get('joint', False))
+  ref = lw(process)
+  process.set_update('gibbs')
+  process.set_thresh('gibbs')
+  process.set_scores('hastings')          # the reference runs Hastings
+  assert process._thresh == 'hastings' and process._update == 'hastings'
+  assert _same_spec(lw(process), ref)
+  process.set_update('gibbs')
+  process.set_thresh('hastings')          # overwrites the update again
+  assert process._update == 'hastings'
+  assert _same_spec(lw(process), ref)
+  process.set_scores(None)
+  assert process._thresh == 'hastings' and process._update == 'hastings'
+  for setter in (process.set_scores, process.set_thresh, process.set_update):
+    with pytest.raises(AssertionError):
+      setter('hastings', 1.)
+    with pytest.raises(AssertionError):
+      setter('metropolis', pscale='log')
+
+
+def test_registry_functions_with_arguments_refused():
+  """A registry function object wrapped with arguments computes something
+  else in the reference (Expression(fn, *args, **kwds), sp.py:67, 84, 100):
+  thresh with limits draws np.random.uniform(lo, hi); scores with a
+  positional pscale; these raise NotLowerable instead of lowering silently.
+  A function from another module named sp_utils is a custom callable."""
+  process, *_ = _build('metrohast_norm1d')
+  with pytest.raises(pb.NotLowerable):
+    process.set_thresh(_registry_fn('metropolis_thresh'), 0.2, 0.9)
+  with pytest.raises(pb.NotLowerable):
+    process.set_thresh(_registry_fn('hastings_thresh'), low=0.2)
+  with pytest.raises(pb.NotLowerable):
+    process.set_scores(_registry_fn('metropolis_scores'), 'log')
+  with pytest.raises(pb.NotLowerable):
+    process.set_update(_registry_fn('hastings_update'), 1)
+  process.set_scores(_registry_fn('metropolis_scores'), pscale='log')
+  assert process._scores == 'metropolis' and process._scores_pscale == 'log'
+  imposter = _registry_fn('metropolis_scores')
+  imposter.__module__ = 'myproj.sp_utils'
+  with pytest.raises(pb.NotLowerable):
+    process.set_scores(imposter, pscale='log')
