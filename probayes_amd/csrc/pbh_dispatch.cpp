@@ -493,17 +493,17 @@ __device__ __forceinline__ int block_min(int v, int *red) {
   return min(min(red[0], red[1]), min(red[2], red[3]));
 }
 
-__global__ __launch_bounds__(kFftT) __attribute__((amdgpu_waves_per_eu(3, 3)))
-void trace_ess_fft_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
-                          int32_t T, double *ess) {
-  __shared__ double sb[kFftN + kFftN / 16];
-  __shared__ double red[8];
-  __shared__ int ired[8];
-  // XCD-aware pair index: block b runs on XCD b % 8; give each XCD a
-  // contiguous range of pairs
+// XCD-aware pair index: block b runs on XCD b % 8; give each XCD a
+// contiguous range of pairs
+__device__ __forceinline__ int64_t xcd_pair_index() {
   const int64_t nb = gridDim.x, b = blockIdx.x;
   const int64_t per = nb / 8, rem = nb % 8, xcd = b % 8, idx = b / 8;
-  const int64_t P = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
+__device__ __forceinline__ void ess4k_pair(const double *tx, int64_t n, int32_t d,
+                                           int64_t first, int32_t T, double *ess,
+                                           int64_t P, double *sb, double *red, int *ired) {
   const int64_t S = (int64_t)d * n;
   const int64_t s0 = 2 * P;
   const bool has_b = s0 + 1 < S;
@@ -629,11 +629,537 @@ void trace_ess_fft_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
   }
 }
 
+__global__ __launch_bounds__(kFftT) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void trace_ess_fft_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
+                          int32_t T, double *ess) {
+  __shared__ double sb[kFftN + kFftN / 16];
+  __shared__ double red[8];
+  __shared__ int ired[8];
+  ess4k_pair(tx, n, d, first, T, ess, xcd_pair_index(), sb, red, ired);
+}
+
+// The 4 096-point form over a device list of pairs (the 2 048-point kernel's
+// fallback: list[0] = count, pairs in list[1 ..]): one block per possible
+// entry, the blocks past the count exit at once.  (A fixed grid striding over
+// the list kept every block's registers live across iterations: 289 spilled
+// VGPRs.)
+__global__ __launch_bounds__(kFftT) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void trace_ess_fft_list_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
+                               int32_t T, double *ess, const int32_t *list) {
+  __shared__ double sb[kFftN + kFftN / 16];
+  __shared__ double red[8];
+  __shared__ int ired[8];
+  const int32_t cnt = __builtin_nontemporal_load(list);   // block-uniform
+  if ((int32_t)blockIdx.x >= cnt) return;
+  ess4k_pair(tx, n, d, first, T, ess, list[1 + blockIdx.x], sb, red, ired);
+}
+
+// ---------------------------------------------------------------------------
+// The 2 048-point form (round 5): the same estimator with the pair's complex
+// series zero-padded to N = 2 048 instead of 4 096.  The circular
+// autocovariance at lag k is then a_k + a_{N-k}, and a_{N-k} = 0 while N - k
+// >= T: lags k <= N - T are exact.  Geyer's scan needs lags up to its first
+// non-positive pair, which for the cfg5 chains (T = 1 500, exact to lag 548)
+// is at lag ~180 at the median and beyond 548 for ~1 % of the series (a
+// NumPy simulation of the cfg5 target); a pair whose scan reaches the end of
+// the exact range without a non-positive pair is appended to a device list
+// and redone by the 4 096-point form (trace_ess_fft_list_kernel).  Half the
+// points per transform (and one pass of radix 8 instead of 16): 128 threads
+// x 16 points, radix 16, 16, 8.  The radix-8 pass leaves thread j holding
+// X[j + 128 q] in natural order, so the spectrum's unpack and the inverse's
+// first pass read and write the registers in place.
+// ---------------------------------------------------------------------------
+constexpr int kF2N = 2048, kF2T = 128;
+
+template <int SIGN>
+__device__ __forceinline__ void dft8(cdbl &a0, cdbl &a1, cdbl &a2, cdbl &a3, cdbl &a4,
+                                     cdbl &a5, cdbl &a6, cdbl &a7) {
+  // X[2k] = DFT4(a_n + a_{n+4})[k], X[2k+1] = DFT4((a_n - a_{n+4}) W8^n)[k]
+  constexpr double C2 = 0.70710678118654752440;
+  cdbl b0 = cadd(a0, a4), b1 = cadd(a1, a5), b2 = cadd(a2, a6), b3 = cadd(a3, a7);
+  cdbl c0 = csub(a0, a4), c1 = csub(a1, a5), c2 = csub(a2, a6), c3 = csub(a3, a7);
+  // W8 = (C2, SIGN C2): c1 W8, c2 (SIGN i), c3 W8^3 = (-C2, SIGN C2)
+  c1 = cdbl{C2 * (c1.re - SIGN * c1.im), C2 * (c1.im + SIGN * c1.re)};
+  c2 = cmuli<SIGN>(c2);
+  c3 = cdbl{-C2 * (c3.re + SIGN * c3.im), C2 * (SIGN * c3.re - c3.im)};
+  dft4<SIGN>(b0, b1, b2, b3);
+  dft4<SIGN>(c0, c1, c2, c3);
+  a0 = b0; a2 = b1; a4 = b2; a6 = b3;
+  a1 = c0; a3 = c1; a5 = c2; a7 = c3;
+}
+
+// pass 3 (NS = 256, radix 8): thread j runs DFTs j and j + 128 over its
+// even / odd points (x[m + 256 r] = v[2 r] or v[2 r + 1]), twiddles w^r with
+// w = exp(SIGN 2 pi i m / 2048); outputs land in natural order, v[q] = X[j + 128 q]
+template <int SIGN>
+__device__ __forceinline__ void fft2_pass3(cdbl (&v)[16], cdbl wa) {
+  constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173;
+  const cdbl wb = cmul(wa, cdbl{C1, SIGN * S1});   // m + 128: one more 1/16 turn
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const cdbl w = h ? wb : wa;
+    const cdbl w2 = cmul(w, w), w3 = cmul(w2, w), w4 = cmul(w2, w2);
+    v[2 + h] = cmul(v[2 + h], w);
+    v[4 + h] = cmul(v[4 + h], w2);
+    v[6 + h] = cmul(v[6 + h], w3);
+    v[8 + h] = cmul(v[8 + h], w4);
+    v[10 + h] = cmul(v[10 + h], cmul(w4, w));
+    v[12 + h] = cmul(v[12 + h], cmul(w4, w2));
+    v[14 + h] = cmul(v[14 + h], cmul(w4, w3));
+    dft8<SIGN>(v[h], v[2 + h], v[4 + h], v[6 + h], v[8 + h], v[10 + h], v[12 + h], v[14 + h]);
+  }
+}
+
+// pass outputs (fft_out<NS>, 128 threads) to the next pass's inputs
+// x[j + 128 r] in v[r], through sb: real parts then imaginary parts
+template <int NS>
+__device__ __forceinline__ void fft2_exchange(double *sb, cdbl (&v)[16]) {
+  const int j = (int)threadIdx.x;
+  double t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<NS>(i))] = v[i].re;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] = sb[fsw(j + r * kF2T)];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sb[fsw(fft_out<NS>(i))] = v[i].im;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = cdbl{t[r], sb[fsw(j + r * kF2T)]};
+  __syncthreads();
+}
+
+// the whole 2 048-point transform, natural order in and out (v[q] = x[j + 128 q])
+template <int SIGN>
+__device__ __forceinline__ void fft2k(double *sb, cdbl (&v)[16], cdbl w16, cdbl w2k) {
+  fft_compute<SIGN, 1>(v, cdbl{1., 0.});
+  fft2_exchange<1>(sb, v);
+  fft_compute<SIGN, 16>(v, w16);
+  fft2_exchange<16>(sb, v);
+  fft2_pass3<SIGN>(v, w2k);
+}
+
+__device__ __forceinline__ double block2_sum(double v, double *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1];
+}
+__device__ __forceinline__ int block2_min(int v, int *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return min(red[0], red[1]);
+}
+
+// T <= kF2N - 2 records; list[0] counts the pairs handed to the 4 096-point
+// form, list[1 ..] holds them (list[0] zeroed before the launch)
+__global__ __launch_bounds__(kF2T) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void trace_ess_fft2k_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
+                            int32_t T, double *ess, int32_t *list) {
+  __shared__ double sb[kF2N + kF2N / 16];
+  __shared__ double red[4];
+  __shared__ int ired[4];
+  const int64_t P = xcd_pair_index();
+  const int64_t S = (int64_t)d * n;
+  const int64_t s0 = 2 * P;
+  const bool has_b = s0 + 1 < S;
+  const int j = (int)threadIdx.x;
+  const int64_t row = S;
+  const double *src = tx + first * row + s0;
+  // ---- load (t = j + 128 q) and centre ----
+  cdbl v[16];
+  double sa = 0., sbb = 0.;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int t = j + q * kF2T;
+    v[q] = cdbl{0., 0.};
+    if (t < T) {
+      if (has_b && !(row & 1)) {
+        const double2 x = *reinterpret_cast<const double2 *>(src + (int64_t)t * row);
+        v[q] = cdbl{x.x, x.y};
+      } else if (has_b) {   // odd d n: every other record is 8-byte aligned
+        v[q] = cdbl{src[(int64_t)t * row], src[(int64_t)t * row + 1]};
+      } else {
+        v[q] = cdbl{src[(int64_t)t * row], 0.};
+      }
+    }
+    sa += v[q].re;
+    sbb += v[q].im;
+  }
+  const double ma = block2_sum(sa, red) / (double)T;
+  const double mb = block2_sum(sbb, red + 2) / (double)T;
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+    if (j + q * kF2T < T) v[q] = cdbl{v[q].re - ma, has_b ? v[q].im - mb : 0.};
+  // twiddle bases: pass 2 exp(-2 pi i (j % 16) / 256), pass 3 exp(-2 pi i j / 2048)
+  cdbl w16, w2k;
+  {
+    double sn, cs;
+    sincospi(-(double)(2 * (j % 16)) / 256.0, &sn, &cs);
+    w16 = cdbl{cs, sn};
+    sincospi(-(double)(2 * j) / 2048.0, &sn, &cs);
+    w2k = cdbl{cs, sn};
+  }
+  fft2k<-1>(sb, v, w16, w2k);
+  // ---- unpack Z_k, Z_{N-k} (k = j + 128 q) and pack |X_k|^2 + i |Y_k|^2:
+  // imaginary parts first, so that only their squares stay live (48 doubles
+  // at the peak instead of 64) ----
+  {
+    double xi2[16], yr2[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sb[fsw(j + q * kF2T)] = v[q].im;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = j + q * kF2T;
+      const double zk = v[q].im, zm = sb[fsw((kF2N - k) & (kF2N - 1))];
+      const double xi = zk - zm, yr = zk + zm;   // 2 Im X_k, 2 Re Y_k
+      xi2[q] = xi * xi;
+      yr2[q] = yr * yr;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sb[fsw(j + q * kF2T)] = v[q].re;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = j + q * kF2T;
+      const double zk = v[q].re, zm = sb[fsw((kF2N - k) & (kF2N - 1))];
+      const double xr = zk + zm, yi = zm - zk;   // 2 Re X_k, 2 Im Y_k
+      v[q] = cdbl{__builtin_fma(xr, xr, xi2[q]), __builtin_fma(yi, yi, yr2[q])};
+    }
+    __syncthreads();
+  }
+  fft2k<1>(sb, v, conj(w16), conj(w2k));
+  // ---- lags 0 .. 1023 of both series to LDS (a: [0, 1088), b: [1088, ...)) ----
+  constexpr int kB = kF2N / 2 + kF2N / 32;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = fsw(j + q * kF2T);
+    sb[e] = v[q].re;
+    sb[kB + e] = v[q].im;
+  }
+  __syncthreads();
+  // ---- Geyer's initial positive sequence over the exact pairs ----
+  const double a0 = sb[0], b0 = sb[kB];
+  const double ia = 1.0 / (a0 > 1e-300 ? a0 : 1e-300);
+  const double ib = 1.0 / (b0 > 1e-300 ? b0 : 1e-300);
+  const int m = (T - 1) / 2;          // pairs (lags 2J + 1, 2J + 2), J < m
+  const int mx = (kF2N - T) / 2;      // pairs whose lags are all <= N - T
+  const int lim = m < mx ? m : mx;    // <= 511: lags <= 1023
+  double pa[4], pb[4];
+  int fa = lim, fb = lim;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int J = j + q * kF2T;
+    pa[q] = pb[q] = 0.;
+    if (J < lim) {
+      const int e1 = fsw(2 * J + 1), e2 = fsw(2 * J + 2);
+      pa[q] = sb[e1] * ia + sb[e2] * ia;
+      pb[q] = sb[kB + e1] * ib + sb[kB + e2] * ib;
+      if (pa[q] <= 0. && J < fa) fa = J;
+      if (pb[q] <= 0. && J < fb) fb = J;
+    }
+  }
+  fa = block2_min(fa, ired);
+  fb = block2_min(fb, ired + 2);
+  // a scan that ran to the end of the exact range short of m: the 4 096-point
+  // form decides this pair
+  const bool redo = lim < m && (fa == lim || (has_b && fb == lim));
+  if (redo) {
+    if (j == 0) {
+      const int32_t at = __hip_atomic_fetch_add(list, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      list[1 + at] = (int32_t)P;
+    }
+    return;   // block-uniform
+  }
+  double qa = 0., qb = 0.;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int J = j + q * kF2T;
+    if (J < fa) qa += pa[q];
+    if (J < fb) qb += pb[q];
+  }
+  qa = block2_sum(qa, red);
+  qb = block2_sum(qb, red + 2);
+  if (j == 0) {
+    const double da = 1.0 + 2.0 * qa, db = 1.0 + 2.0 * qb;
+    ess[s0] = (double)T / (da > 1e-12 ? da : 1e-12);
+    if (has_b) ess[s0 + 1] = (double)T / (db > 1e-12 ? db : 1e-12);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The 2 048-point form on ONE wavefront per pair (the default): 64 lanes x 32
+// points, the same radix 16, 16, 8 passes (two 16-point DFTs per lane in the
+// first two, four 8-point DFTs in the third).  A one-wave workgroup has no
+// barriers (the compiler drops them): its exchanges through LDS wait only on
+// the wave's own accesses, and a SIMD's two waves never wait for each other
+// (the two-wave form spent 41 % of its wave cycles parked at barriers and
+// waits, r05a_ess).  The spectrum's unpack pairs lane j with lane 64 - j
+// through ds_bpermute (Z_{N-k} for k = j + 64 r is lane 64 - j's point 31 -
+// r; lane 0's is its own point 32 - r), in place, so no extra registers.
+// ---------------------------------------------------------------------------
+constexpr int kWL = 64;   // lanes
+
+// exchange for the one-wave form: outputs (v[i] at lds index out(i)) to
+// natural order x[j + 64 r] in v[r], real parts then imaginary parts
+template <typename OUT>
+__device__ __forceinline__ void fftw_exchange(double *sb, cdbl (&v)[32], OUT out) {
+  // the real parts come back into the registers they left (in natural order,
+  // while the imaginary parts still sit in pass order): no temporaries
+  const int j = (int)threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) sb[fsw(out(i))] = v[i].re;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 32; ++r) v[r].re = sb[fsw(j + r * kWL)];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 32; ++i) sb[fsw(out(i))] = v[i].im;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 32; ++r) v[r].im = sb[fsw(j + r * kWL)];
+  __syncthreads();
+}
+
+// passes 1 and 2 (radix 16, NS = 1 / 16): DFTs m = j + 64 h, h = 0, 1, over
+// x[m + 128 r'] = v[2 r' + h]; outputs k of DFT h land in v[2 i + h] with
+// i = 4 k1 + k2 for k = k1 + 4 k2 (dft16's order)
+template <int SIGN, int NS>
+__device__ __forceinline__ void fftw_pass16(cdbl (&v)[32], cdbl w) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    cdbl u[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) u[r] = v[2 * r + h];
+    fft_compute<SIGN, NS>(u, w);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[2 * i + h] = u[i];
+  }
+}
+template <int NS>
+struct FftwOut {   // where v[2 i + h] of fftw_pass16<., NS> belongs
+  int j;
+  __device__ __forceinline__ int operator()(int e) const {
+    const int h = e & 1, i = e >> 1;
+    const int m = j + kWL * h, k = (i >> 2) + 4 * (i & 3);
+    return (m / NS) * NS * 16 + (m % NS) + k * NS;
+  }
+};
+
+// pass 3 (radix 8, NS = 256): DFTs m = j + 64 h, h < 4, over x[m + 256 r'] =
+// v[h + 4 r']; twiddles w_m^r' with w_m = w_j exp(SIGN 2 pi i h / 32); outputs
+// in place and natural: v[h + 4 k] = X[m + 256 k] = X[j + 64 (h + 4 k)]
+template <int SIGN>
+__device__ __forceinline__ void fftw_pass3(cdbl (&v)[32], cdbl wj) {
+  // exp(SIGN 2 pi i h / 32), h = 1, 2, 3
+  constexpr double c1 = 0.98078528040323044913, s1 = 0.19509032201612826785;
+  constexpr double c2 = 0.92387953251128675613, s2 = 0.38268343236508977173;
+  constexpr double c3 = 0.83146961230254523708, s3 = 0.55557023301960222474;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const cdbl w = h == 0 ? wj
+                 : cmul(wj, h == 1 ? cdbl{c1, SIGN * s1} : h == 2 ? cdbl{c2, SIGN * s2}
+                                                          : cdbl{c3, SIGN * s3});
+    const cdbl w2 = cmul(w, w), w3 = cmul(w2, w), w4 = cmul(w2, w2);
+    v[4 + h] = cmul(v[4 + h], w);
+    v[8 + h] = cmul(v[8 + h], w2);
+    v[12 + h] = cmul(v[12 + h], w3);
+    v[16 + h] = cmul(v[16 + h], w4);
+    v[20 + h] = cmul(v[20 + h], cmul(w4, w));
+    v[24 + h] = cmul(v[24 + h], cmul(w4, w2));
+    v[28 + h] = cmul(v[28 + h], cmul(w4, w3));
+    dft8<SIGN>(v[h], v[4 + h], v[8 + h], v[12 + h], v[16 + h], v[20 + h], v[24 + h], v[28 + h]);
+  }
+}
+
+template <int SIGN>
+__device__ __forceinline__ void fftw(double *sb, cdbl (&v)[32], cdbl w16, cdbl w2k) {
+  const int j = (int)threadIdx.x;
+  fftw_pass16<SIGN, 1>(v, cdbl{1., 0.});
+  fftw_exchange(sb, v, FftwOut<1>{j});
+  fftw_pass16<SIGN, 16>(v, w16);
+  fftw_exchange(sb, v, FftwOut<16>{j});
+  fftw_pass3<SIGN>(v, w2k);
+}
+
+__device__ __forceinline__ double bperm_f64(int addr, double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// 4 |X_k|^2 + 4 i |Y_k|^2 from z = Z_k and m = Z_{N-k} (X = (Z_k + conj
+// Z_{N-k}) / 2, Y = (Z_k - conj Z_{N-k}) / 2i)
+__device__ __forceinline__ cdbl ess_power(cdbl z, cdbl m) {
+  const double xr = z.re + m.re, xi = z.im - m.im;   // 2 Re X, 2 Im X
+  const double yr = z.im + m.im, yi = m.re - z.re;   // 2 Re Y, 2 Im Y
+  return cdbl{__builtin_fma(xr, xr, xi * xi), __builtin_fma(yr, yr, yi * yi)};
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+
+// T <= 1 536 records (then v[24 ..] start at 0); list as trace_ess_fft2k_kernel
+__global__ __launch_bounds__(kWL) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void trace_ess_fftw_kernel(const double *tx, int64_t n, int32_t d, int64_t first,
+                           int32_t T, double *ess, int32_t *list) {
+  __shared__ double sb[kF2N + kF2N / 16];
+  const int64_t P = xcd_pair_index();
+  const int64_t S = (int64_t)d * n;
+  const int64_t s0 = 2 * P;
+  const bool has_b = s0 + 1 < S;
+  const int j = (int)threadIdx.x;
+  const double *src = tx + first * S + s0;
+  cdbl v[32];
+  double sa = 0., sbb = 0.;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    const int t = j + r * kWL;
+    v[r] = cdbl{0., 0.};
+    if (r < 24 && t < T) {
+      if (has_b && !(S & 1)) {
+        const double2 x = *reinterpret_cast<const double2 *>(src + (int64_t)t * S);
+        v[r] = cdbl{x.x, x.y};
+      } else if (has_b) {   // odd d n: every other record is 8-byte aligned
+        v[r] = cdbl{src[(int64_t)t * S], src[(int64_t)t * S + 1]};
+      } else {
+        v[r] = cdbl{src[(int64_t)t * S], 0.};
+      }
+    }
+    sa += v[r].re;
+    sbb += v[r].im;
+  }
+  const double ma = wave_sum(sa) / (double)T;
+  const double mb = wave_sum(sbb) / (double)T;
+#pragma unroll
+  for (int r = 0; r < 24; ++r)
+    if (j + r * kWL < T) v[r] = cdbl{v[r].re - ma, has_b ? v[r].im - mb : 0.};
+  cdbl w16, w2k;
+  {
+    double sn, cs;
+    sincospi(-(double)(2 * (j % 16)) / 256.0, &sn, &cs);
+    w16 = cdbl{cs, sn};
+    sincospi(-(double)(2 * j) / 2048.0, &sn, &cs);
+    w2k = cdbl{cs, sn};
+  }
+  fftw<-1>(sb, v, w16, w2k);
+  // ---- unpack in place: pairs (i, 31 - i) with lane 64 - j; lane 0 pairs
+  // (i, 32 - i) within itself (and its point 16 alone) ----
+  {
+    const int addr = ((kWL - j) & (kWL - 1)) * 4;
+    const bool l0 = j == 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const cdbl ra{bperm_f64(addr, v[31 - i].re), bperm_f64(addr, v[31 - i].im)};
+      const cdbl rb{bperm_f64(addr, v[i].re), bperm_f64(addr, v[i].im)};
+      const cdbl ma_ = l0 ? v[(32 - i) & 31] : ra;   // Z_{N-k} of point i
+      const cdbl p1 = ess_power(v[i], ma_);
+      const cdbl p2 = ess_power(v[31 - i], rb);
+      // branch-free (a divergent branch per pair kept both paths' copies
+      // of the points live: 99 spilled VGPRs)
+      v[i] = p1;
+      v[31 - i] = cdbl{l0 ? v[31 - i].re : p2.re, l0 ? v[31 - i].im : p2.im};
+      if (i > 0)   // lane 0: P_{N-k} = P_k
+        v[32 - i] = cdbl{l0 ? p1.re : v[32 - i].re, l0 ? p1.im : v[32 - i].im};
+    }
+    const cdbl p16 = ess_power(v[16], v[16]);
+    v[16] = cdbl{l0 ? p16.re : v[16].re, l0 ? p16.im : v[16].im};
+  }
+  fftw<1>(sb, v, conj(w16), conj(w2k));
+  // ---- lags 0 .. 1023 of both series to LDS (a: [0, 1088), b: [1088, ...)) ----
+  constexpr int kB = kF2N / 2 + kF2N / 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int e = fsw(j + r * kWL);
+    sb[e] = v[r].re;
+    sb[kB + e] = v[r].im;
+  }
+  __syncthreads();
+  const double a0 = sb[0], b0 = sb[kB];
+  const double ia = 1.0 / (a0 > 1e-300 ? a0 : 1e-300);
+  const double ib = 1.0 / (b0 > 1e-300 ? b0 : 1e-300);
+  const int m = (T - 1) / 2;
+  const int mx = (kF2N - T) / 2;
+  const int lim = m < mx ? m : mx;   // <= 511
+  double pa[8], pb[8];
+  int fa = lim, fb = lim;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int J = j + q * kWL;
+    pa[q] = pb[q] = 0.;
+    if (J < lim) {
+      const int e1 = fsw(2 * J + 1), e2 = fsw(2 * J + 2);
+      pa[q] = sb[e1] * ia + sb[e2] * ia;
+      pb[q] = sb[kB + e1] * ib + sb[kB + e2] * ib;
+      if (pa[q] <= 0. && J < fa) fa = J;
+      if (pb[q] <= 0. && J < fb) fb = J;
+    }
+  }
+  fa = wave_min(fa);
+  fb = wave_min(fb);
+  if (lim < m && (fa == lim || (has_b && fb == lim))) {
+    if (j == 0) {
+      const int32_t at = __hip_atomic_fetch_add(list, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      list[1 + at] = (int32_t)P;
+    }
+    return;
+  }
+  double qa = 0., qb = 0.;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int J = j + q * kWL;
+    if (J < fa) qa += pa[q];
+    if (J < fb) qb += pb[q];
+  }
+  qa = wave_sum(qa);
+  qb = wave_sum(qb);
+  if (j == 0) {
+    const double da = 1.0 + 2.0 * qa, db = 1.0 + 2.0 * qb;
+    ess[s0] = (double)T / (da > 1e-12 ? da : 1e-12);
+    if (has_b) ess[s0 + 1] = (double)T / (db > 1e-12 ? db : 1e-12);
+  }
+}
+
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
-                            hipStream_t st, bool fft) {
+                            hipStream_t st, int fft, int32_t *list) {
+  const int64_t pairs = ((int64_t)d * n + 1) / 2;
+  // the 2 048-point form while its exact range covers at least 512 lags
+  // (2: one wave per pair, 3: two waves per pair)
+  if ((fft == 2 || fft == 3) && list && count <= kF2N - 512) {
+    hipError_t err = hipMemsetAsync(list, 0, sizeof(int32_t), st);
+    if (err != hipSuccess) return err;
+    if (fft == 2)
+      hipLaunchKernelGGL(trace_ess_fftw_kernel, dim3((unsigned)pairs), dim3(kWL), 0, st,
+                         tx, n, d, first, (int32_t)count, ess, list);
+    else
+      hipLaunchKernelGGL(trace_ess_fft2k_kernel, dim3((unsigned)pairs), dim3(kF2T), 0, st,
+                         tx, n, d, first, (int32_t)count, ess, list);
+    err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(trace_ess_fft_list_kernel, dim3((unsigned)pairs), dim3(kFftT), 0, st,
+                       tx, n, d, first, (int32_t)count, ess, list);
+    return hipGetLastError();
+  }
   if (fft && count <= kFftN / 2) {
-    const int64_t pairs = ((int64_t)d * n + 1) / 2;
     hipLaunchKernelGGL(trace_ess_fft_kernel, dim3((unsigned)pairs), dim3(kFftT), 0, st,
                        tx, n, d, first, (int32_t)count, ess);
     return hipGetLastError();

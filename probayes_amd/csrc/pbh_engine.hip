@@ -73,6 +73,10 @@ struct pbh_engine {
   double *bm64 = nullptr;
   double *lgtab = nullptr;     // legacy_log_table (device legacy streams)
   double *ess = nullptr;     // [d][n] per-chain ESS (pbh_trace_ess), NaN before
+  int32_t *ess_list = nullptr;   // the 2 048-point ESS form's fallback list
+  int64_t ess_list_len = 0;
+  double *ess_host = nullptr;    // pinned staging of the ESS copy-out
+  int64_t ess_host_len = 0;
   bool spin_sync = true;     // poll <= 2 ms, then block; PBH_SYNC=block: block
   bool sync_event = false;   // PBH_SYNC=event: poll the last run's end event
   // timing events as marker packets around the launches (default), or
@@ -81,7 +85,7 @@ struct pbh_engine {
   // ~7 us more wall per short launch, measured: profiles/r02j_events.jsonl)
   bool gmm_full = true;      // PBH_GMM_FULL=0: no steady-state quad kernel
   bool pair_full = true;     // PBH_PAIR_FULL=0: no steady-state pair kernel
-  bool ess_fft = true;       // PBH_ESS_FFT=0: the direct-sum ESS kernel
+  int ess_fft = 2;           // PBH_ESS_FFT=1: the 4 096-point form only, 0: direct sums
   bool iid_full = true;      // PBH_IID_FULL=0: no steady-state iid kernel
   bool iid_pair = false;     // PBH_IID_PAIR=1: the steady-state iid kernel on lane pairs (measured slower)
   int fair = 11;             // PBH_FAIR=k: wave priorities alternate every 2^k x 10 ns (0: off)
@@ -245,7 +249,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
-  if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef) != 0;
+  if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef);
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *fp = std::getenv("PBH_IID_PAIR")) e->iid_pair = std::atoi(fp) != 0;
   if (const char *fa = std::getenv("PBH_FAIR")) e->fair = std::min(20, std::max(0, std::atoi(fa)));
@@ -292,7 +296,8 @@ int pbh_destroy(pbh_engine *e) {
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
-  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab);
+  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab); dfree(e->ess_list);
+  if (e->ess_host) (void)hipHostFree(e->ess_host);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1377,12 +1382,32 @@ int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
     return fail(PBH_ERR_ARG, "ESS needs >= 2 records inside [0, %lld), got [%lld, %lld)",
                 (long long)rec, (long long)first, (long long)(first + count));
   HIP_TRY(hipSetDevice(e->device));
+  const int64_t dn = (int64_t)e->d * e->n;
+  if (e->ess_fft >= 2 && e->ess_list_len < (dn + 1) / 2 + 1) {
+    dfree(e->ess_list);
+    e->ess_list_len = 0;
+    HIP_TRY(hipMalloc(&e->ess_list, ((dn + 1) / 2 + 1) * sizeof(int32_t)));
+    e->ess_list_len = (dn + 1) / 2 + 1;
+  }
   HIP_TRY(pbh::launch_trace_ess(e->tx, e->n, e->d, first, count, e->ess, e->stream,
-                                e->ess_fft));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  if (ess)
-    HIP_TRY(hipMemcpy(ess, e->ess, (size_t)e->d * e->n * sizeof(double),
-                      hipMemcpyDeviceToHost));
+                                e->ess_fft, e->ess_list));
+  if (ess) {
+    // through a pinned staging buffer: a pageable copy of the 512 KB cfg5
+    // result was ~0.1 ms of the call
+    if (e->ess_host_len < dn) {
+      if (e->ess_host) (void)hipHostFree(e->ess_host);
+      e->ess_host = nullptr;
+      e->ess_host_len = 0;
+      HIP_TRY(hipHostMalloc(&e->ess_host, dn * sizeof(double), hipHostMallocDefault));
+      e->ess_host_len = dn;
+    }
+    HIP_TRY(hipMemcpyAsync(e->ess_host, e->ess, dn * sizeof(double), hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    std::memcpy(ess, e->ess_host, dn * sizeof(double));
+  } else {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
   return PBH_OK;
 }
 

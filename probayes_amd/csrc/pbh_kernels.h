@@ -159,10 +159,13 @@ hipError_t launch_trace_expectation(const double *tx, const double *tlp,
                                     int64_t n, int32_t d, int64_t first,
                                     int64_t count, double exponent, int32_t lin,
                                     double log_npi, double *out, hipStream_t s);
-// fft: the FFT form for count <= 2048 records (else the direct-sum kernel)
+// fft: 2 = the 2 048-point FFT form for count <= 1 536 records with the
+// 4 096-point form for the pairs it cannot decide (list: (d n + 1) / 2 + 1
+// int32 of device scratch), 1 = the 4 096-point form for count <= 2 048
+// records, 0 (or a longer trace) = the direct-sum kernel
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
-                            hipStream_t st, bool fft = true);
+                            hipStream_t st, int fft, int32_t *list);
 // Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
 void bm64_tables(double *out);
 // the legacy generator's log table (pbh_legacy.hip log_leg): 129 rows of

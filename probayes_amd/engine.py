@@ -465,7 +465,7 @@ class Engine:
     out = np.empty((self.dim, self.n))
     _lib.call('pbh_trace_ess', self._h, _c.c_int64(int(first)),
               _c.c_int64(int(count)), _dp(out))
-    return out.T.copy()
+    return out.T   # a [N, d] view of the [d][N] result (no 2-D transpose copy)
 
   def trace_expectation(self, first=0, count=None, exponent=None):
     """PD.expectation (pd.py:373-405) of the summary of trace records

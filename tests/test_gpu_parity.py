@@ -256,27 +256,43 @@ def _ess_ips(x):
   return t / np.maximum(1.0 + 2.0 * s, 1e-12), pairs, first
 
 
-@pytest.mark.parametrize('fft', ['1', '0'])
-@pytest.mark.parametrize('name,n,t,burn', [('gmm2', 2000, 600, 100),
-                                           ('diag10', 300, 257, 7),
-                                           ('gmm2', 33, 2100, 40),
-                                           # odd d n: unaligned series pairs
-                                           ('mcmc_prob2', 33, 300, 10),
-                                           ('bound_list3', 33, 300, 10),
-                                           # the FFT kernel's edges: exactly
-                                           # 2 048 records (half its 4 096
-                                           # points), and 13 records
-                                           ('gmm2', 64, 2058, 10),
-                                           ('diag10', 40, 23, 10)])
-def test_device_ess_and_trace_stats_match_host(monkeypatch, name, n, t, burn, fft):
-  """pbh_trace_ess (on-device initial positive sequence: the FFT kernel,
-  or with PBH_ESS_FFT=0 the direct-sum kernel; more than 2 048 records
-  always take the direct sums) equals the host FFT estimator on the same
-  trace within 1e-9 wherever the sequence's stopping pair is not within
-  rounding of zero; pbh_trace_stats equals the host sums of the trace."""
+@pytest.mark.parametrize('fft', ['2', '3', '1', '0'])
+@pytest.mark.parametrize('name,n,t,burn,scale', [('gmm2', 2000, 600, 100, None),
+                                                 ('diag10', 300, 257, 7, None),
+                                                 ('gmm2', 33, 2100, 40, None),
+                                                 # odd d n: unaligned series pairs
+                                                 ('mcmc_prob2', 33, 300, 10, None),
+                                                 ('bound_list3', 33, 300, 10, None),
+                                                 # the FFT kernels' edges: exactly
+                                                 # 2 048 records (half the 4 096
+                                                 # points), 1 536 (the 2 048-point
+                                                 # form's last length), 1 537, and
+                                                 # 13 records
+                                                 ('gmm2', 64, 2058, 10, None),
+                                                 ('gmm2', 64, 1546, 10, None),
+                                                 ('gmm2', 64, 1547, 10, None),
+                                                 ('diag10', 40, 23, 10, None),
+                                                 # cfg5's record count: ~1 % of the
+                                                 # pairs need lags past 548
+                                                 ('gmm2', 2000, 2000, 500, None),
+                                                 # slow mixing: most pairs' scans
+                                                 # run past the 2 048-point form's
+                                                 # exact lags (its fallback list)
+                                                 ('gmm2', 300, 1400, 100, 0.05),
+                                                 ('diag10', 65, 1300, 10, 0.02)])
+def test_device_ess_and_trace_stats_match_host(monkeypatch, name, n, t, burn, scale, fft):
+  """pbh_trace_ess (on-device initial positive sequence: the 2 048-point FFT
+  kernel with the 4 096-point one for the pairs whose scan leaves its exact
+  lags (PBH_ESS_FFT=2, the default), the 4 096-point kernel alone (1), or the
+  direct-sum kernel (0); more than 2 048 records always take the direct sums)
+  equals the host FFT estimator on the same trace within 1e-9 wherever the
+  sequence's stopping pair is not within rounding of zero; pbh_trace_stats
+  equals the host sums of the trace."""
   from probayes_amd import Engine
   monkeypatch.setenv('PBH_ESS_FFT', fft)
   spec = oracle.golden_spec(name)
+  if scale is not None:
+    spec['proposal']['scale'] = np.full_like(spec['proposal']['scale'], scale)
   eng = Engine(spec)
   eng.init_chains(golden_init(name, n))
   eng.set_rng('philox', seed=17)
@@ -285,6 +301,7 @@ def test_device_ess_and_trace_stats_match_host(monkeypatch, name, n, t, burn, ff
   eng.run(t, steps_per_launch=100)
   tr = eng.trace()
   dev = eng.trace_ess(burn)
+  assert np.array_equal(dev, eng.trace_ess(burn))   # the fallback list resets
   st = eng.trace_stats(burn)
   eng.close()
   x = tr['v_x'][:, burn:]
