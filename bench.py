@@ -260,6 +260,52 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
   return out
 
 
+def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup,
+                    spl):
+  """The parity-carrying mode on the same cfg2 shape:
+  REPLAY -- the kernels read one NumPy RandomState(global chain id) stream
+  per chain, generated on the device (pbh_legacy_seed / pbh_legacy_replay:
+  MT19937 + the polar legacy gauss, the reference's per-step draw order), and
+  run the reference's arithmetic, so chains equal the reference CPU path's.
+  Timed like the headline (barrier + sync on both sides, max over ranks):
+  stream generation and the replay launches of exactly `steps` steps, the
+  full trace written.  Returns chain-steps/s of the whole job (not `value`)."""
+  from probayes_amd.dist import shard
+  offset, n = shard(chains_per_gpu * world, rank, world)
+  eng = make_engine()
+  eng.init_chains(np.zeros((n, D)), chain_offset=offset)
+  eng.set_rng('replay')
+  eng.seed_legacy(offset + np.arange(n))
+  eng.alloc_trace(warmup + steps, 1)
+  chunk = max(1, min(spl, steps))
+
+  def advance(k):
+    done = 0
+    while done < k:
+      m = min(chunk, k - done)
+      eng.legacy_replay(m)   # the next m rows of every chain's stream
+      eng.run(m, sync=False)
+      done += m
+
+  def barrier():
+    eng.sync()
+    if col is not None:
+      col.allreduce_max(0.0)
+
+  if warmup:
+    advance(warmup)
+  barrier()
+  t0 = time.perf_counter()
+  advance(steps)
+  eng.sync()
+  el = time.perf_counter() - t0
+  barrier()
+  if col is not None:
+    el = col.allreduce_max(el)
+  eng.close()
+  return float(chains_per_gpu) * world * steps / el, el
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
@@ -281,6 +327,8 @@ def main():
                   'of <= 16 steps, else --steps-per-launch)')
   ap.add_argument('--traffic-bytes', type=float, default=None,
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
+  ap.add_argument('--no-replay', action='store_true',
+                  help='skip the reference-identical REPLAY line fields')
   args = ap.parse_args()
 
   world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -319,6 +367,12 @@ def main():
                  spl, args.rng, trace=not args.no_trace, moments=args.moments,
                  warmup_spl=args.warmup_spl)
   n, el, kern_ms, launches = res['n'], res['el'], res['kern_ms'], res['launches']
+  replay = None
+  if not args.no_replay:
+    # after the headline's timed region and its collection, on a fresh engine
+    replay = run_replay_rank(lambda: Engine(cfg2_spec(), device=local), col, rank,
+                             world, args.chains, args.steps, args.warmup,
+                             min(spl, 250))
   collect_ms = res.get('collect_ms')
   if 'stats' in res:   # every chain of every rank, once
     assert int(res['stats']['counts'].sum()) == args.chains * world
@@ -364,6 +418,16 @@ def main():
     }
     if collect_ms is not None:
       line['rccl_allgather_ms'] = collect_ms
+    if replay is not None:
+      # the parity mode (reference-identical chains), same shape and clock;
+      # reported beside value, never folded into it
+      line['replay_chain_steps_per_s'] = replay[0]
+      line['replay_ms_per_step'] = replay[1] * 1e3 / args.steps
+      line['replay_config'] = ('REPLAY: per-chain NumPy RandomState(global '
+                               'chain id) streams generated on the device '
+                               '(MT19937 + polar legacy gauss) and the '
+                               'reference arithmetic; stream generation '
+                               'inside the timed region')
     if cpu is not None:
       line['cpu_baseline'] = cpu
     print(json.dumps(line), flush=True)

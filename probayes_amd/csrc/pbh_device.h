@@ -407,6 +407,28 @@ __device__ __forceinline__ void bm64_load(double *lds, const double *g) {
 // row {-2 ln c, 1/c}; q4 is -2 log1p(r) / r to degree 4.
 struct LogTerm { double r, T; int e; };
 
+// Timing-only A/B build (never shipped, wrong numbers):
+// -DPBH_LDS_AB replaces every table lookup's LDS offset by a lane-based one
+// (lane x the entry size: consecutive entries, no two lanes of a lookup in
+// the same bank) that still depends on the original offset (v_and with 0,
+// v_add: one VALU more per lookup, so the loads stay in place).  The values
+// read are wrong but valid table entries, so the chains keep their ranges and
+// the filters their rare exact paths.  (A wave-uniform offset through
+// v_readfirstlane serialised every lookup on an SGPR round trip: 0.27 ->
+// 0.39 ms per 250-step launch, not a conflict measurement.)
+#ifdef PBH_LDS_AB
+template <int ENTRY>
+__device__ __forceinline__ uint32_t lds_ab(uint32_t off) {
+  uint32_t r;
+  asm volatile("v_and_b32 %0, 0, %1\n\tv_add_u32 %0, %0, %2"
+               : "=&v"(r) : "v"(off), "v"((uint32_t)(threadIdx.x & 63u) * ENTRY));
+  return r;
+}
+#else
+template <int ENTRY>
+__device__ __forceinline__ uint32_t lds_ab(uint32_t off) { return off; }
+#endif
+
 __device__ __forceinline__ uint32_t bfe_6_15(uint32_t v) {
   // v_bfe_u32 v, 6, 15 as written (LLVM turns a bfe of a masked value into a
   // shift and a second mask, one VALU more)
@@ -421,7 +443,7 @@ __device__ __forceinline__ LogTerm log_term(double x, const double *tab) {
   const uint32_t ch = (hi32(m) + 0x200u) & 0xFFFFFC00u;            // c (hi word)
   // row j = (ch - 0x3FE00000) >> 10: byte offset 16 j = bits [20:6] of ch
   const double2 lt = *reinterpret_cast<const double2 *>(
-      reinterpret_cast<const char *>(tab + kBm64LogOff) + bfe_6_15(ch));
+      reinterpret_cast<const char *>(tab + kBm64LogOff) + lds_ab<16>(bfe_6_15(ch)));
   return LogTerm{(m - from_words(ch, 0u)) * lt.y, lt.x, e};
 }
 
@@ -451,7 +473,7 @@ __device__ __forceinline__ void bm96_pair(uint32_t a, uint32_t b, uint32_t c,
   const double ee = __builtin_fma(-tt, yr, 1.0);
   const double rr = __builtin_fma(tt * ee, __builtin_fma(ee, 0.375, 0.5), tt);
   // ---- (sin, cos) of the full-turn angle ----
-  const char *sct = reinterpret_cast<const char *>(tab) + (b & 0xFFCu);
+  const char *sct = reinterpret_cast<const char *>(tab) + lds_ab<4>(b & 0xFFCu);
   const uint32_t *scw = reinterpret_cast<const uint32_t *>(sct);
   const double2 sc{from_words(scw[kBm64ScN], scw[0]),
                    from_words(scw[3 * kBm64ScN], scw[2 * kBm64ScN])};
@@ -494,7 +516,7 @@ __device__ __forceinline__ double exp_tab(double y, const double *tab) {
   p = __builtin_fma(p, r, 1.0);
   p = __builtin_fma(p, r, 1.0);
   const int ki = (int)k;
-  const double t = tab[kBm64ExpOff + (ki & 63)];
+  const double t = tab[kBm64ExpOff + lds_ab<1>((uint32_t)ki & 63u)];
   return __builtin_ldexp(t * p, ki >> 6);
 }
 

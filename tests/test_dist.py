@@ -307,8 +307,13 @@ class MainEngine(OracleEngine):
     s, q, a = self.stats
     blk, counts = self.col.allgather_stats(s, q, a)
     return unpack_stats(blk, counts, bench.D)
+  def seed_legacy(self, seeds):
+    assert len(seeds) == len(self.x0) and seeds[0] == self.off
+  def legacy_replay(self, k):
+    assert k >= 1
   def close(self):
-    self.col.close()
+    if getattr(self, 'col', None) is not None:
+      self.col.close()
 
 
 probayes_amd.Engine = MainEngine        # main() imports it from the package
@@ -333,6 +338,7 @@ if rank == 0:
   assert line['roofline']['bound'] == 'hbm' and line['roofline']['frac'] > 0
   assert line['config']['parallelism'] == 'chain-sharded x{{}}'.format(world)
   assert line['scaling'] == 'weak'
+  assert line['replay_chain_steps_per_s'] > 0 and 'REPLAY' in line['replay_config']
   print('MAIN_OK')
 else:
   assert out == '', out
