@@ -248,8 +248,12 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
   el = time.perf_counter() - t0
   kern_ms, launches = eng.last_run_ms()
   barrier()
+  server = None
+  if hasattr(eng, 'server_info'):
+    server = eng.server_info()
+    eng.stop_server()   # nothing else on this device waits behind it
   out = {'n': n, 'offset': offset, 'el': el, 'kern_ms': kern_ms,
-         'launches': launches, 'enqueue_s': t1 - t0}
+         'launches': launches, 'enqueue_s': t1 - t0, 'server': server}
   if col is not None:
     out['el'] = col.allreduce_max(el)
     t1 = time.perf_counter()
@@ -349,6 +353,10 @@ def main():
   # completion signals (hipDeviceScheduleSpin, process-wide, opt-in at
   # pbh_create; a short launch is seen to end ~2 us sooner)
   os.environ.setdefault('PBH_SPIN_FLAG', '1')
+  # the resident sampling server (pbh_server_*): each timed run is a command
+  # to a kernel launched during the warm-up (the steady-state lane-pair
+  # kernel, chain state in registers); PBH_SERVER=0 launches per run
+  os.environ.setdefault('PBH_SERVER', '1')
   from probayes_amd import Engine
   eng = Engine(cfg2_spec(), device=local)
   col = None
@@ -410,6 +418,13 @@ def main():
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),
+        # resident server: the timed run was a command to a kernel launched in
+        # the warm-up; its kernel time is the command's device time (first
+        # workgroup's sight of it to the last one's completion, s_memrealtime)
+        'server': res.get('server'),
+        'timing': ('device stamps of the resident server command'
+                   if res.get('server') and res['server'].get('commands')
+                   else 'HIP events around the launches'),
         # where the timed region's wall time went (rank 0): the host enqueue
         # of the launches, the HIP-event time of the launches
         'host_enqueue_us': res['enqueue_s'] * 1e6,

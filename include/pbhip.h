@@ -267,8 +267,27 @@ int pbh_sync(pbh_engine *eng);
  * kernels keep no running moments (no per-launch read-modify-write of them);
  * pbh_trace_stats then reduces the recorded trace on the device instead.   */
 int pbh_set_collect(pbh_engine *eng, int32_t flags);
-/* Kernel-only time of the last pbh_run (HIP events on the engine stream). */
+/* Kernel-only time of the last pbh_run (HIP events on the engine stream;
+ * for a resident-server command, its first workgroup's sight of the command
+ * to its last workgroup's completion on the device's 100 MHz clock).       */
 int pbh_last_run_ms(pbh_engine *eng, double *ms, int64_t *launches);
+/* Resident sampling server (opt-in, PBH_SERVER=1 at pbh_create; the
+ * walk/next loop of sp.py:221-295 kept resident on the device): a run that is
+ * one steady-state lane-pair launch (the cfg2 form, production Philox, thin
+ * 1, past step 1, every record inside the trace) becomes a command to a
+ * kernel that stays resident with the chain state in registers; the kernel
+ * leaves after PBH_SERVER_IDLE_MS (default 1000) without a command.  Every
+ * other entry point stops it first; pbh_server_stop stops it explicitly
+ * (chain state stored, stream idle); pbh_destroy stops it.  active = the
+ * server kernel is running; commands / launches: totals of this engine.    */
+int pbh_server_stop(pbh_engine *eng);
+int pbh_server_info(pbh_engine *eng, int32_t *active, int64_t *commands,
+                    int64_t *launches);
+/* Diagnostic: the server's per-workgroup completion words of the last
+ * command (seq, the 100 MHz stamps of its sight and completion); n = the
+ * workgroup count, at most cap entries copied.                             */
+int pbh_server_stamps(pbh_engine *eng, int32_t cap, uint32_t *seq, uint64_t *t0,
+                      uint64_t *t1, int32_t *n);
 
 /* ---- results (SP.__call__(samples) summary: sp.py:131-198) -------------- */
 int pbh_get_state(pbh_engine *eng, double *x, double *logp);

@@ -84,6 +84,21 @@ hipError_t launch_mh(const KArgs &a, hipStream_t s, size_t lds) {
   }
 }
 
+template <int D>
+hipError_t launch_mh_server_d(const KArgs &a, hipStream_t st, int32_t *wgs, bool check);
+
+hipError_t launch_mh_server(const KArgs &a, hipStream_t s, int32_t *wgs, bool check) {
+  switch (a.d) {
+#define PBH_CASE(D) \
+  case D:           \
+    return launch_mh_server_d<D>(a, s, wgs, check);
+    PBH_DIMS(PBH_CASE)
+#undef PBH_CASE
+    default:
+      return hipErrorNotSupported;
+  }
+}
+
 hipError_t launch_gibbs(const KArgs &a, hipStream_t s) {
   switch (a.d) {
 #define PBH_CASE(D) \

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <string>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <vector>
 
@@ -114,6 +115,21 @@ struct pbh_engine {
   // timing of the last pbh_run
   bool timed = false;
   int64_t last_launches = 0;
+  // resident sampling server (PBH_SERVER=1; pbh_server_*): the FULL pair
+  // kernel launched once, each eligible pbh_run a command in pinned host
+  // memory; srv_timed: the last run was a command (timed by its stamps)
+  bool srv_enabled = false;
+  bool srv_active = false;
+  bool srv_timed = false;
+  uint32_t srv_seq = 0, srv_pending = 0;
+  int32_t srv_wgs = 0;
+  int64_t srv_idle_ms = 1000;      // PBH_SERVER_IDLE_MS: the kernel's idle exit
+  pbh::SrvCmd *srv_cmd = nullptr;  // pinned, fine-grained
+  pbh::SrvDone *srv_done = nullptr;
+  pbh::SrvCmd *srv_mail = nullptr;   // device memory: workgroup 0's relay
+  int32_t srv_done_len = 0;
+  std::chrono::steady_clock::time_point srv_last{};
+  int64_t srv_commands = 0, srv_launches = 0;
   // RCCL
   ncclComm_t comm = nullptr;
   int32_t rank = 0, world = 1;
@@ -201,6 +217,130 @@ void free_trace(pbh_engine *e) {
 
 extern "C" {
 
+// ---------------------------------------------------------------------------
+// Resident sampling server (PBH_SERVER=1, bench.py's default): the FULL pair
+// kernel launched once per series of eligible runs (mh_pair_kernel<..., SRV>)
+// keeps the chain state in registers and the tables in LDS; each pbh_run is a
+// command in pinned host memory, each workgroup reports (seq, stamps).
+// Invariants: one command in flight; a command is written only when the
+// previous one completed and the host has been idle for less than half the
+// kernel's idle exit (so no workgroup can have left on its own); every entry
+// point that touches the device state, the trace or the stream stops the
+// server first (SRV_STOP); pbh_sync never syncs the stream while it runs;
+// pbh_destroy stops it.
+// ---------------------------------------------------------------------------
+namespace {
+using srv_clk = std::chrono::steady_clock;
+
+bool srv_kernel_ended(pbh_engine *e) { return hipStreamQuery(e->stream) == hipSuccess; }
+
+bool srv_all_done(const pbh_engine *e, uint32_t seq) {
+  for (int32_t w = 0; w < e->srv_wgs; ++w)
+    if (__atomic_load_n(&e->srv_done[w].seq, __ATOMIC_ACQUIRE) != seq) return false;
+  return true;
+}
+
+// every workgroup reported `seq`; ok_if_ended: an ended kernel is no error
+// (the exit command: workgroups that left idle do not acknowledge it)
+int srv_wait(pbh_engine *e, uint32_t seq, bool ok_if_ended) {
+  const auto t0 = srv_clk::now();
+  for (uint64_t it = 1;; ++it) {
+    if (srv_all_done(e, seq)) return PBH_OK;
+    if ((it & 1023) == 0) {
+      if (srv_kernel_ended(e)) {
+        if (srv_all_done(e, seq) || ok_if_ended) return PBH_OK;
+        return fail(PBH_ERR_HIP, "sampling server ended before command %u completed", seq);
+      }
+      if (srv_clk::now() - t0 > std::chrono::seconds(120))
+        return fail(PBH_ERR_HIP, "sampling server: command %u not completed in 120 s", seq);
+    }
+  }
+}
+
+int srv_stop(pbh_engine *e) {
+  if (!e->srv_active) return PBH_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = PBH_OK;
+  if (e->srv_pending) {
+    rc = srv_wait(e, e->srv_pending, false);
+    e->srv_pending = 0;
+  }
+  if (!srv_kernel_ended(e)) {
+    const uint32_t q = ++e->srv_seq;
+    e->srv_cmd->op = pbh::kSrvExit;
+    __atomic_store_n(&e->srv_cmd->seq, q, __ATOMIC_RELEASE);
+    const int rc2 = srv_wait(e, q, true);
+    if (!rc) rc = rc2;
+  }
+  const hipError_t err = hipStreamSynchronize(e->stream);
+  e->srv_active = false;
+  if (!rc && err != hipSuccess)
+    rc = fail(PBH_ERR_HIP, "sampling server exit: %s", hipGetErrorString(err));
+  return rc;
+}
+
+int srv_launch(pbh_engine *e, pbh::KArgs k) {
+  int32_t wgs = 0;
+  hipError_t err = pbh::launch_mh_server(k, e->stream, &wgs, true);
+  if (err != hipSuccess) return fail(PBH_ERR_UNSUPPORTED, "no resident server form");
+  if (!e->srv_cmd) {
+    err = hipHostMalloc((void **)&e->srv_cmd, sizeof(pbh::SrvCmd), hipHostMallocCoherent);
+    if (err != hipSuccess) {
+      e->srv_cmd = nullptr;
+      return fail(PBH_ERR_HIP, "server command block: %s", hipGetErrorString(err));
+    }
+  }
+  if (e->srv_done_len < wgs) {
+    if (e->srv_done) (void)hipHostFree(e->srv_done);
+    e->srv_done = nullptr;
+    e->srv_done_len = 0;
+    err = hipHostMalloc((void **)&e->srv_done, (size_t)wgs * sizeof(pbh::SrvDone),
+                        hipHostMallocCoherent);
+    if (err != hipSuccess) {
+      e->srv_done = nullptr;
+      return fail(PBH_ERR_HIP, "server completion words: %s", hipGetErrorString(err));
+    }
+    e->srv_done_len = wgs;
+  }
+  if (!e->srv_mail) {
+    err = hipMalloc((void **)&e->srv_mail, sizeof(pbh::SrvCmd));
+    if (err != hipSuccess) {
+      e->srv_mail = nullptr;
+      return fail(PBH_ERR_HIP, "server mailbox: %s", hipGetErrorString(err));
+    }
+  }
+  // the previous server (if any) has ended: sequence numbers restart
+  HIP_TRY(hipMemsetAsync(e->srv_mail, 0, sizeof(pbh::SrvCmd), e->stream));
+  std::memset(e->srv_done, 0, (size_t)wgs * sizeof(pbh::SrvDone));
+  std::memset(e->srv_cmd, 0, sizeof(pbh::SrvCmd));
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  e->srv_seq = 0;
+  void *dcmd = nullptr, *ddone = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dcmd, e->srv_cmd, 0));
+  HIP_TRY(hipHostGetDevicePointer(&ddone, e->srv_done, 0));
+  k.srv_cmd = dcmd;
+  k.srv_done = ddone;
+  k.srv_mail = e->srv_mail;
+  k.srv_idle = e->srv_idle_ms * 100000;   // 10 ns ticks
+  err = pbh::launch_mh_server(k, e->stream, &wgs, false);
+  if (err != hipSuccess) return fail(PBH_ERR_HIP, "server launch: %s", hipGetErrorString(err));
+  e->srv_wgs = wgs;
+  e->srv_active = true;
+  e->srv_last = srv_clk::now();
+  ++e->srv_launches;
+  return PBH_OK;
+}
+}  // namespace
+
+#define SRV_STOP(e)                        \
+  do {                                     \
+    if ((e)->srv_active) {                 \
+      const int srv_rc_ = srv_stop(e);     \
+      if (srv_rc_) return srv_rc_;         \
+    }                                      \
+  } while (0)
+
+
 const char *pbh_last_error(void) { return g_err.c_str(); }
 
 int pbh_abi_version(void) { return PBH_ABI_VERSION; }
@@ -249,6 +389,9 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *em = std::getenv("PBH_EVENT_MARKERS")) e->event_markers = std::atoi(em) != 0;
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
+  if (const char *sv = std::getenv("PBH_SERVER")) e->srv_enabled = sv[0] == '1';
+  if (const char *si = std::getenv("PBH_SERVER_IDLE_MS"))
+    e->srv_idle_ms = std::max<int64_t>(1, std::min<int64_t>(10000, std::atoll(si)));
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef);
   if (const char *fi = std::getenv("PBH_IID_FULL")) e->iid_full = std::atoi(fi) != 0;
   if (const char *fp = std::getenv("PBH_IID_PAIR")) e->iid_pair = std::atoi(fp) != 0;
@@ -287,6 +430,7 @@ int pbh_create(int device, pbh_engine **out) {
 int pbh_destroy(pbh_engine *e) {
   if (!e) return PBH_OK;
   (void)hipSetDevice(e->device);
+  if (e->srv_active) (void)srv_stop(e);   // never leave the server running
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
@@ -298,6 +442,9 @@ int pbh_destroy(pbh_engine *e) {
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
   dfree(e->bm64); dfree(e->ess); dfree(e->lgtab); dfree(e->ess_list);
   if (e->ess_host) (void)hipHostFree(e->ess_host);
+  if (e->srv_cmd) (void)hipHostFree(e->srv_cmd);
+  if (e->srv_done) (void)hipHostFree(e->srv_done);
+  dfree(e->srv_mail);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -310,6 +457,7 @@ int pbh_destroy(pbh_engine *e) {
 // ---------------------------------------------------------------------------
 int pbh_set_model(pbh_engine *e, const pbh_model *m) {
   if (check_ptr(e, "engine") || check_ptr(m, "model")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   const int d = m->dim;
   if (d < 1 || d > PBH_MAX_DIM)
     return fail(PBH_ERR_ARG, "dim %d outside 1..%d", d, PBH_MAX_DIM);
@@ -456,6 +604,7 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
 
 int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
   if (check_ptr(e, "engine") || check_ptr(p, "proposal")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
   const int d = e->d;
   std::vector<double> blk;
@@ -556,6 +705,7 @@ int pbh_set_proposal(pbh_engine *e, const pbh_proposal *p) {
 
 int pbh_set_gibbs(pbh_engine *e, const pbh_gibbs *gb) {
   if (check_ptr(e, "engine") || check_ptr(gb, "gibbs")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
   if (e->k.target != PBH_TARGET_MVN || e->k.scores != PBH_SCORES_GIBBS)
     return fail(PBH_ERR_UNSUPPORTED,
@@ -632,6 +782,7 @@ int pbh_set_gibbs(pbh_engine *e, const pbh_gibbs *gb) {
 // ---------------------------------------------------------------------------
 int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   if (check_ptr(e, "engine") || check_ptr(init, "init")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->has_model) return fail(PBH_ERR_STATE, "pbh_set_model first");
   if (n < 1 || off < 0) return fail(PBH_ERR_ARG, "bad n_chains/offset");
   // kernels address a chain's trace word through a 32-bit buffer offset
@@ -682,6 +833,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
 
 int pbh_set_step(pbh_engine *e, int64_t g) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (e->has_pred || e->cap > 0 || e->rep)
     return fail(PBH_ERR_STATE, "pbh_set_step goes right after pbh_init_chains");
@@ -692,6 +844,7 @@ int pbh_set_step(pbh_engine *e, int64_t g) {
 
 int pbh_set_rng(pbh_engine *e, int32_t mode, uint64_t seed) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (mode != PBH_RNG_REPLAY && mode != PBH_RNG_PHILOX &&
       mode != PBH_RNG_PHILOX_F64 && mode != PBH_RNG_XOSHIRO &&
       mode != PBH_RNG_PHILOX_FP32)
@@ -712,6 +865,7 @@ int pbh_stream_width(pbh_engine *e, int32_t *r) {
 
 int pbh_upload_replay(pbh_engine *e, int64_t n_steps, const double *rand) {
   if (check_ptr(e, "engine") || check_ptr(rand, "rand")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   int32_t R = 0;
   int rc = pbh_stream_width(e, &R);
@@ -743,6 +897,7 @@ int pbh_upload_replay(pbh_engine *e, int64_t n_steps, const double *rand) {
 
 int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   if (check_ptr(e, "engine") || check_ptr(seeds, "seeds")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   const int64_t n = e->n;
   HIP_TRY(hipSetDevice(e->device));
@@ -774,6 +929,7 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
 
 int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first");
   if (e->mt_stale)
     return fail(PBH_ERR_STATE, "pbh_restore ran after pbh_legacy_seed: set the "
@@ -847,6 +1003,7 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
 int pbh_get_replay(pbh_engine *e, int64_t first, int64_t n_steps, int32_t draw,
                    double *out) {
   if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->rep) return fail(PBH_ERR_STATE, "no replay stream");
   if (first < 0 || n_steps < 0 || first + n_steps > e->rep_steps)
     return fail(PBH_ERR_ARG, "rows [%lld, %lld) outside the %lld-row stream",
@@ -884,6 +1041,7 @@ int pbh_get_replay(pbh_engine *e, int64_t first, int64_t n_steps, int32_t draw,
 // ---------------------------------------------------------------------------
 int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (capacity < 0 || thin < 1) return fail(PBH_ERR_ARG, "bad capacity/thin");
   HIP_TRY(hipSetDevice(e->device));
@@ -1043,6 +1201,73 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
                       k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
                          ? (size_t)k.tn * sizeof(double) : 0;
+  // the resident server: one command for the whole run when the run is one
+  // steady-state lane-pair launch (launch_mh_server's check); anything else
+  // stops a running server and launches normally
+  if (e->srv_enabled && !e->has_gibbs && spl >= n_steps && n_steps <= (1 << 30)) {
+    pbh::KArgs kc = k;
+    kc.g0 = e->g;
+    kc.n_steps = (int32_t)n_steps;
+    kc.has_pred = e->has_pred ? 1 : 0;
+    const bool short_run = n_steps <= 64;
+    kc.fair = short_run ? e->fair_short : e->fair;
+    kc.fair_rel = short_run ? 1 : e->fair_rel;
+    kc.srv_cmd = kc.srv_done = kc.srv_mail = reinterpret_cast<void *>(1);   // the check only
+    int32_t wgs = 0;
+    // a running server's form (model, proposal, RNG, trace) was checked at
+    // its launch -- every entry point that changes them stops it -- so only
+    // this run's own shape is checked (no occupancy query per command)
+    const bool form = e->srv_active
+        ? (!k.moments && e->has_pred && e->cap > 0 && e->thin == 1 &&
+           e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap)
+        : pbh::launch_mh_server(kc, e->stream, &wgs, true) == hipSuccess;
+    if (form) {
+      if (e->srv_active) {
+        if (e->srv_pending) {   // one command in flight
+          const int rc = srv_wait(e, e->srv_pending, false);
+          e->srv_pending = 0;
+          e->srv_last = srv_clk::now();
+          if (rc) return rc;
+        }
+        // a server that has ended, or whose idle exit could be near, is
+        // replaced: a command never races the kernel's own exit
+        const auto idle = srv_clk::now() - e->srv_last;
+        // (the stream query only after a pause: back-to-back commands cannot
+        // have seen the kernel leave, and srv_wait notices a faulted one)
+        if (idle > std::chrono::milliseconds(e->srv_idle_ms / 2) ||
+            (idle > std::chrono::milliseconds(1) && srv_kernel_ended(e))) {
+          const int rc = srv_stop(e);
+          if (rc) return rc;
+        }
+      }
+      if (!e->srv_active) {
+        const int rc = srv_launch(e, kc);
+        if (rc) return rc;
+      }
+      pbh::SrvCmd *cmd = e->srv_cmd;
+      cmd->op = pbh::kSrvRun;
+      cmd->g0 = e->g;
+      cmd->n = (int32_t)n_steps;
+      cmd->fair = kc.fair;
+      cmd->fair_rel = kc.fair_rel;
+      const uint32_t q = ++e->srv_seq;
+      __atomic_store_n(&cmd->seq, q, __ATOMIC_RELEASE);
+      e->srv_pending = q;
+      e->srv_last = srv_clk::now();
+      e->g += n_steps;
+      e->has_pred = true;
+      e->mom_steps += n_steps;
+      e->timed = true;
+      e->srv_timed = true;
+      e->last_launches = 1;
+      ++e->srv_commands;
+      tq("server command");
+      return PBH_OK;
+    }
+    (void)hipGetLastError();
+  }
+  SRV_STOP(e);
+  e->srv_timed = false;
   // the timed region: events on the first / last dispatch packet, or (with
   // PBH_EVENT_MARKERS=1) separate marker packets around the launches
   pbh::LaunchEvents &lev = pbh::launch_events();
@@ -1092,6 +1317,15 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
 int pbh_sync(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   HIP_TRY(hipSetDevice(e->device));
+  if (e->srv_active) {   // never the stream: the server kernel is on it
+    if (e->srv_pending) {
+      const int rc = srv_wait(e, e->srv_pending, false);
+      e->srv_pending = 0;
+      e->srv_last = std::chrono::steady_clock::now();
+      return rc;
+    }
+    return PBH_OK;
+  }
   if (e->spin_sync) {
     // poll the stream for up to 2 ms: a short launch's completion is seen
     // within a microsecond or so (a blocking wait sleeps on the completion
@@ -1133,6 +1367,22 @@ int pbh_last_run_ms(pbh_engine *e, double *ms, int64_t *launches) {
     if (launches) *launches = 0;
     return PBH_OK;
   }
+  if (e->srv_timed) {
+    // the last run was a server command: the first workgroup's sight of it
+    // to the last workgroup's completion, on the 100 MHz real-time clock
+    if (e->srv_active && e->srv_pending) {
+      const int rc = pbh_sync(e);
+      if (rc) return rc;
+    }
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (int32_t w = 0; w < e->srv_wgs; ++w) {
+      t0 = std::min<uint64_t>(t0, __atomic_load_n(&e->srv_done[w].t0, __ATOMIC_ACQUIRE));
+      t1 = std::max<uint64_t>(t1, __atomic_load_n(&e->srv_done[w].t1, __ATOMIC_ACQUIRE));
+    }
+    *ms = t1 > t0 ? (double)(t1 - t0) * 1e-5 : 0.;
+    if (launches) *launches = e->last_launches;
+    return PBH_OK;
+  }
   HIP_TRY(hipEventSynchronize(e->ev1));
   float f = 0.f;
   HIP_TRY(hipEventElapsedTime(&f, e->ev0, e->ev1));
@@ -1141,11 +1391,38 @@ int pbh_last_run_ms(pbh_engine *e, double *ms, int64_t *launches) {
   return PBH_OK;
 }
 
+int pbh_server_stop(pbh_engine *e) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  return PBH_OK;
+}
+
+int pbh_server_info(pbh_engine *e, int32_t *active, int64_t *commands, int64_t *launches) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  if (active) *active = e->srv_active && !srv_kernel_ended(e) ? 1 : 0;
+  if (commands) *commands = e->srv_commands;
+  if (launches) *launches = e->srv_launches;
+  return PBH_OK;
+}
+
+int pbh_server_stamps(pbh_engine *e, int32_t cap, uint32_t *seq, uint64_t *t0,
+                      uint64_t *t1, int32_t *n) {
+  if (check_ptr(e, "engine") || check_ptr(n, "n")) return PBH_ERR_ARG;
+  *n = e->srv_done ? e->srv_wgs : 0;
+  for (int32_t w = 0; w < *n && w < cap; ++w) {
+    if (seq) seq[w] = __atomic_load_n(&e->srv_done[w].seq, __ATOMIC_ACQUIRE);
+    if (t0) t0[w] = __atomic_load_n(&e->srv_done[w].t0, __ATOMIC_ACQUIRE);
+    if (t1) t1[w] = __atomic_load_n(&e->srv_done[w].t1, __ATOMIC_ACQUIRE);
+  }
+  return PBH_OK;
+}
+
 // ---------------------------------------------------------------------------
 // results
 // ---------------------------------------------------------------------------
 int pbh_get_state(pbh_engine *e, double *x, double *logp) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1186,6 +1463,8 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
                 int32_t has_pred, const uint32_t *xo) {
   if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
     return PBH_ERR_ARG;
+  SRV_STOP(e);
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
   if (e->rng == PBH_RNG_XOSHIRO && !xo)
@@ -1221,6 +1500,7 @@ int pbh_set_chains(pbh_engine *e, const double *x, const double *lp,
                    int64_t step, int32_t has_pred) {
   if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
     return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
   const int64_t n = e->n;
@@ -1252,6 +1532,7 @@ int pbh_get_legacy_state(pbh_engine *e, uint32_t *key, int32_t *pos,
   if (check_ptr(e, "engine") || check_ptr(key, "key") || check_ptr(pos, "pos") ||
       check_ptr(has, "has") || check_ptr(gauss, "gauss"))
     return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->mt_key) return fail(PBH_ERR_STATE, "no legacy streams (pbh_legacy_seed)");
   if (e->mt_stale) return fail(PBH_ERR_STATE, "legacy state stale after pbh_restore");
   const int64_t n = e->n;
@@ -1270,6 +1551,7 @@ int pbh_set_legacy_state(pbh_engine *e, const uint32_t *key, const int32_t *pos,
   if (check_ptr(e, "engine") || check_ptr(key, "key") || check_ptr(pos, "pos") ||
       check_ptr(has, "has") || check_ptr(gauss, "gauss"))
     return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first (the layout)");
   const int64_t n = e->n;
   const size_t kw = (size_t)mt_words(e->mt_mode) * n;
@@ -1294,6 +1576,7 @@ int pbh_get_trace(pbh_engine *e, int64_t first, int64_t cnt, double *x,
                   double *logp, uint64_t *acc, double *p_x, double *p_p,
                   double *s) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   int64_t rec = 0;
   pbh_trace_len(e, &rec);
   if (first < 0 || cnt < 0 || first + cnt > rec)
@@ -1317,6 +1600,7 @@ int pbh_get_trace(pbh_engine *e, int64_t first, int64_t cnt, double *x,
 int pbh_get_moments(pbh_engine *e, double *sum, double *sumsq, int64_t *n_acc,
                     int64_t *n_steps) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1331,6 +1615,7 @@ int pbh_get_moments(pbh_engine *e, double *sum, double *sumsq, int64_t *n_acc,
 int pbh_trace_stats(pbh_engine *e, int64_t first, int64_t count, double *sum,
                     double *sumsq, int64_t *n_acc) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   int64_t rec = 0;
   pbh_trace_len(e, &rec);
   if (first < 0 || count < 0 || first + count > rec)
@@ -1352,6 +1637,7 @@ int pbh_trace_stats(pbh_engine *e, int64_t first, int64_t count, double *sum,
 int pbh_trace_expectation(pbh_engine *e, int64_t first, int64_t count,
                           double exponent, double *out) {
   if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   int64_t rec = 0;
   pbh_trace_len(e, &rec);
   if (first < 0 || count < 1 || first + count > rec)
@@ -1376,6 +1662,7 @@ int pbh_trace_expectation(pbh_engine *e, int64_t first, int64_t count,
 
 int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   int64_t rec = 0;
   pbh_trace_len(e, &rec);
   if (first < 0 || count < 2 || first + count > rec)
@@ -1413,6 +1700,7 @@ int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
 
 int pbh_reset_moments(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   HIP_TRY(hipSetDevice(e->device));
   const size_t dn = (size_t)e->d * e->n;
@@ -1438,6 +1726,7 @@ int pbh_rccl_unique_id(uint8_t id[128]) {
 
 int pbh_rccl_init(pbh_engine *e, int32_t rank, int32_t world, const uint8_t id[128]) {
   if (check_ptr(e, "engine") || check_ptr(id, "id")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (world < 1 || rank < 0 || rank >= world) return fail(PBH_ERR_ARG, "bad rank/world");
   HIP_TRY(hipSetDevice(e->device));
   if (e->comm) {
@@ -1514,6 +1803,7 @@ hipError_t keep(hipError_t acc, hipError_t e) { return acc != hipSuccess ? acc :
 
 int pbh_rccl_max_chains(pbh_engine *e, int64_t *n_max) {
   if (check_ptr(e, "engine") || check_ptr(n_max, "n_max")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
   const bool ok = hipSetDevice(e->device) == hipSuccess;
   return rccl_agree(e, ok && e->x != nullptr, e->n, n_max, "pbh_rccl_max_chains");
@@ -1521,6 +1811,7 @@ int pbh_rccl_max_chains(pbh_engine *e, int64_t *n_max) {
 
 int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
   // a bad argument is this rank's failure: it still takes part
   bool ok = out != nullptr && counts != nullptr;
@@ -1581,6 +1872,7 @@ int pbh_rccl_allgather_stats(pbh_engine *e, double *out, int64_t *counts) {
 
 int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
   if (check_ptr(e, "engine") || check_ptr(value, "value")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (!e->comm) return fail(PBH_ERR_STATE, "pbh_rccl_init first");
   // (value, status): the status is rccl_agree's finite vote
   double v[2] = {*value, 0.};
@@ -1605,6 +1897,7 @@ int pbh_rccl_allreduce_max(pbh_engine *e, double *value) {
 
 int pbh_rccl_destroy(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
   if (e->comm) {
     HIP_TRY(hipSetDevice(e->device));
     RCCL_TRY(ncclCommDestroy(e->comm));

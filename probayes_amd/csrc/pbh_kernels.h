@@ -124,6 +124,13 @@ struct KArgs {
   int32_t fair;        // alternate the SIMD's wave priorities every 2^fair real-time ticks (0: off)
   int32_t pair_wg;     // FULL pair kernel's workgroup size (256 or 512)
   int32_t fair_rel;    // FULL pair kernel: the alternation clock starts at the wave's loop entry
+  // resident sampling server (FULL pair kernel, SRV): the host command block
+  // and the per-workgroup completion words (pinned, fine-grained host
+  // memory, SrvCmd / SrvDone), and the idle exit in 10 ns ticks
+  void *srv_cmd;
+  void *srv_done;
+  void *srv_mail;     // device copy of the command (SrvCmd), relayed by workgroup 0
+  int64_t srv_idle;
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;
@@ -131,6 +138,26 @@ struct KArgs {
   // ---- production fp64 normals: bm64 tables (pbh_device.h), global copy
   const double *bm64;
 };
+// The resident server's host command block and completion words (engine:
+// pbh_server_*, kernel: mh_pair_kernel<..., SRV>).  The host writes the
+// fields, then seq (release).  Workgroup 0's first wave alone polls the host
+// block (one PCIe read in flight: 256 workgroups polling host memory at once
+// took ~45 us per read) and relays each command to a device-memory mailbox
+// of the same layout, which every other workgroup's first wave polls; each
+// workgroup runs the command and writes its SrvDone (seq last) to host
+// memory.  op: 0 run, 1 exit.
+struct SrvCmd {
+  uint32_t seq, n;
+  int64_t g0;
+  uint32_t op, fair, fair_rel, pad;
+};
+struct SrvDone {
+  uint32_t seq, pad;
+  uint64_t t0, t1;   // s_memrealtime (100 MHz) when the command was seen / done
+  uint64_t pad2;
+};
+constexpr uint32_t kSrvRun = 0, kSrvExit = 1;
+
 
 // The production Gibbs kernel runs for the Philox RNG without debug records,
 // d <= 16 (its per-lane constant block grows as d^2).
@@ -141,6 +168,9 @@ inline bool gibbs_fast_form(const KArgs &a) {
 // Host launchers (pbh_kernels.hip).
 hipError_t launch_mh(const KArgs &a, hipStream_t s, size_t lds_bytes);
 hipError_t launch_gibbs(const KArgs &a, hipStream_t s);
+// the resident server (FULL lane-pair kernel, SRV): check = only report
+// whether `a` qualifies and the grid is resident at once (wgs: workgroups)
+hipError_t launch_mh_server(const KArgs &a, hipStream_t s, int32_t *wgs, bool check);
 hipError_t launch_xo_seed(uint32_t *xo, int64_t n, int64_t off, uint64_t seed,
                           hipStream_t s);
 bool mh_dim_supported(int d);

@@ -1297,11 +1297,12 @@ __device__ __attribute__((noinline)) bool pair_exact(uint32_t seed_lo, uint32_t 
 // integer/fp64 draw chains with each step's density -> decision -> select
 // chain).  The same words and arithmetic as the general form: identical
 // chains (tests/test_gpu_parity.py).
-template <int D, int RNG, bool MOM, bool LOC0 = false, bool FULL = false>
+template <int D, int RNG, bool MOM, bool LOC0 = false, bool FULL = false, bool SRV = false>
 __global__ __launch_bounds__(FULL ? kPairFullBlock : kBlock)
 __attribute__((amdgpu_waves_per_eu(2)))
 void mh_pair_kernel(KArgs a) {
   static_assert(!FULL || (RNG == PBH_RNG_PHILOX && !MOM), "FULL: production Philox");
+  static_assert(!SRV || FULL, "the resident server runs the steady-state form");
   static_assert(D % 2 == 0, "lane-pair kernel needs even D");
   constexpr int H = D / 2;
   constexpr bool PHX = RNG == PBH_RNG_PHILOX || RNG == PBH_RNG_PHILOX_FP32;
@@ -1562,6 +1563,10 @@ void mh_pair_kernel(KArgs a) {
       }
       if (s < a.n_steps) step(s, cA, ctA, t1);
     } else if constexpr (FULL) {
+        // the launch's (or, SRV, the current command's) first step, step
+        // count and wave-slot alternation
+        int64_t g0v = a.g0;
+        int32_t nsv = a.n_steps, fairv = a.fair, fair_relv = a.fair_rel;
         // ---- steady state: whole pairs (see FULL above the kernel) ----
         constexpr int NW = 3 * H + 1, NB = (NW + 3) / 4, QA = (H + 1) / 2;
         constexpr uint64_t kHi = 0xFFFFFFFF00000000ull;
@@ -1573,7 +1578,7 @@ void mh_pair_kernel(KArgs a) {
         const uint32_t lpbytes = (uint32_t)(a.n * 8);
         const uint32_t aoff = lane == 32 ? (uint32_t)((c >> 5) * 4) : kNoStore;
         const uint32_t abytes = (uint32_t)(a.W * 8);
-        int64_t rec = a.g0 + s - a.rec_base;   // thin 1: record = step
+        int64_t rec = g0v + s - a.rec_base;   // thin 1: record = step
         const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);
         // blocks Q0 .. NB-1 of pair P (the words before block Q0 unused)
         auto philox_from = [&](int64_t P, uint32_t (&w)[4 * NB], auto Q0) {
@@ -1646,7 +1651,7 @@ void mh_pair_kernel(KArgs a) {
           if (needm) {   // wave-uniform, rare
             bool ex = false;
             if (__builtin_amdgcn_inverse_ballot_w64(needm))
-              ex = pair_exact(a.seed_lo, a.seed_hi, a.log_npi, a.g0 + si, chain, h,
+              ex = pair_exact(a.seed_lo, a.seed_hi, a.log_npi, g0v + si, chain, h,
                               t0, lpp, lp);
             accm = (accm & ~needm) | (__ballot(ex) & needm);
           }
@@ -1667,63 +1672,174 @@ void mh_pair_kernel(KArgs a) {
         using I0 = std::integral_constant<int, 0>;
         using IA = std::integral_constant<int, QA>;
         using IH = std::integral_constant<int, H>;
-        if (a.g0 & 1) {   // launch starts on a pair's 2nd step
-          // only step B's normals: Box-Muller pairs H/2 .. H-1 and the lead
-          // word, i.e. the blocks from the one holding word 3 (H / 2) on
-          constexpr int QB = 3 * (H / 2) / 4;
-          uint32_t w[4 * NB];
-          philox_from(a.g0 >> 1, w, std::integral_constant<int, QB>{});
-          normals(w, std::integral_constant<int, H / 2>{}, IH{}, cA, cB);
-          __builtin_amdgcn_s_waitcnt(0);   // the entry loads, before the first step
-          step_full(0, cB, w[3 * H] & 0xFFFFu);
-          s = 1;
-        }
-        if (s + 1 < a.n_steps) {
-          uint32_t w[4 * NB];
-          philox((a.g0 + s) >> 1, w);
-          normals(w, I0{}, IH{}, cA, cB);
-          ctA = w[3 * H] >> 16;
-          ctB = w[3 * H] & 0xFFFFu;
-          if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // no stores in flight yet
-          PBH_PHASE(2);
-          const uint32_t slot = a.fair ? simd_wave_slot() : 0u;
-          // a.fair_rel: the alternation's clock starts at this wave's loop
-          // entry (the waves of a launch start within ~0.4 us of each other),
-          // so the hand-overs of a short launch fall at the same points of
-          // every launch instead of wherever the free-running clock is
-          const uint64_t tfair0 =
-              a.fair_rel ? __builtin_amdgcn_s_memrealtime() : 0ull;
-          for (; s + 3 < a.n_steps; s += 2) {
-            if (a.fair) {
-              const int64_t el = (int64_t)(__builtin_amdgcn_s_memrealtime() - tfair0);
-              fair_prio((uint32_t)((el > 0 ? (uint64_t)el : 0ull) >> a.fair) + slot);
-            }
-            PBH_PHASE_Q(s >> 1, a.n_steps >> 1);
-            uint32_t nw[4 * NB];
-            double nA[H], nB[H];
-            philox(((a.g0 + s) >> 1) + 1, nw);
-            step_full(s, cA, ctA);
-            normals(nw, I0{}, IA{}, nA, nB);
-            step_full(s + 1, cB, ctB);
-            normals(nw, IA{}, IH{}, nA, nB);
-#pragma unroll
-            for (int i = 0; i < H; ++i) {
-              cA[i] = nA[i];
-              cB[i] = nB[i];
-            }
-            ctA = nw[3 * H] >> 16;
-            ctB = nw[3 * H] & 0xFFFFu;
+        // one launch's (one command's) steps [g0v, g0v + nsv)
+        auto run_block = [&]() {
+          if (g0v & 1) {   // launch starts on a pair's 2nd step
+            // only step B's normals: Box-Muller pairs H/2 .. H-1 and the lead
+            // word, i.e. the blocks from the one holding word 3 (H / 2) on
+            constexpr int QB = 3 * (H / 2) / 4;
+            uint32_t w[4 * NB];
+            philox_from(g0v >> 1, w, std::integral_constant<int, QB>{});
+            normals(w, std::integral_constant<int, H / 2>{}, IH{}, cA, cB);
+            __builtin_amdgcn_s_waitcnt(0);   // the entry loads, before the first step
+            step_full(0, cB, w[3 * H] & 0xFFFFu);
+            s = 1;
           }
-          step_full(s, cA, ctA);
-          step_full(s + 1, cB, ctB);
-          s += 2;
-        }
-        if (s < a.n_steps) {   // launch ends on a pair's 1st step
-          uint32_t w[4 * NB];
-          philox((a.g0 + s) >> 1, w);
-          normals(w, I0{}, IA{}, cA, cB);
-          if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // a one-step launch
-          step_full(s, cA, w[3 * H] >> 16);
+          if (s + 1 < nsv) {
+            uint32_t w[4 * NB];
+            philox((g0v + s) >> 1, w);
+            normals(w, I0{}, IH{}, cA, cB);
+            ctA = w[3 * H] >> 16;
+            ctB = w[3 * H] & 0xFFFFu;
+            if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // no stores in flight yet
+            PBH_PHASE(2);
+            const uint32_t slot = fairv ? simd_wave_slot() : 0u;
+            // fair_relv: the alternation's clock starts at this wave's loop
+            // entry (the waves of a launch start within ~0.4 us of each other),
+            // so the hand-overs of a short launch fall at the same points of
+            // every launch instead of wherever the free-running clock is
+            const uint64_t tfair0 =
+                fair_relv ? __builtin_amdgcn_s_memrealtime() : 0ull;
+            for (; s + 3 < nsv; s += 2) {
+              if (fairv) {
+                const int64_t el = (int64_t)(__builtin_amdgcn_s_memrealtime() - tfair0);
+                fair_prio((uint32_t)((el > 0 ? (uint64_t)el : 0ull) >> fairv) + slot);
+              }
+              PBH_PHASE_Q(s >> 1, nsv >> 1);
+              uint32_t nw[4 * NB];
+              double nA[H], nB[H];
+              philox(((g0v + s) >> 1) + 1, nw);
+              step_full(s, cA, ctA);
+              normals(nw, I0{}, IA{}, nA, nB);
+              step_full(s + 1, cB, ctB);
+              normals(nw, IA{}, IH{}, nA, nB);
+  #pragma unroll
+              for (int i = 0; i < H; ++i) {
+                cA[i] = nA[i];
+                cB[i] = nB[i];
+              }
+              ctA = nw[3 * H] >> 16;
+              ctB = nw[3 * H] & 0xFFFFu;
+            }
+            step_full(s, cA, ctA);
+            step_full(s + 1, cB, ctB);
+            s += 2;
+          }
+          if (s < nsv) {   // launch ends on a pair's 1st step
+            uint32_t w[4 * NB];
+            philox((g0v + s) >> 1, w);
+            normals(w, I0{}, IA{}, cA, cB);
+            if (s == 0) __builtin_amdgcn_s_waitcnt(0);   // a one-step launch
+            step_full(s, cA, w[3 * H] >> 16);
+          }
+        };
+        if constexpr (SRV) {
+          // ---- resident sampling server (engine pbh_server_*): the chain
+          // state stays in registers and the tables in LDS across commands.
+          // Thread 0 of each workgroup polls the host command block (pinned,
+          // fine-grained memory, uncached system-scope loads); the other
+          // waves wait at the barrier.  After a command, every wave's stores
+          // have left (vmcnt 0), and thread 0 writes the workgroup's
+          // completion word with (seq, start, end) real-time stamps through
+          // vector system-scope stores.  No command for srv_idle ticks (or
+          // an exit command) ends the loop: the epilogue stores x and lp.
+          // (wave 0 of the workgroup polls as a whole wave -- the same
+          // address in every lane, one request -- and writes the same values
+          // from every lane: no divergent branch around the step code, whose
+          // lane masks must stay in SGPRs)
+          __shared__ int64_t s_cmd[6];
+          SrvCmd *const hcmd = reinterpret_cast<SrvCmd *>(a.srv_cmd);
+          SrvCmd *const mail = reinterpret_cast<SrvCmd *>(a.srv_mail);
+          SrvDone *const donep = reinterpret_cast<SrvDone *>(a.srv_done) + blockIdx.x;
+          const bool poller = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == 0;
+          const bool relay = blockIdx.x == 0;   // the one host poller
+          uint32_t seen = 0u;
+          for (;;) {
+            if (poller) {
+              const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+              // workgroup 0 reads the host block (system scope, uncached);
+              // the others the device mailbox (agent scope)
+              SrvCmd *const src = relay ? hcmd : mail;
+              uint32_t q;
+              for (;;) {
+                q = relay ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+                                &src->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                          : (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+                                &src->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (q != seen) break;
+                if (__builtin_amdgcn_s_memrealtime() - tw > (uint64_t)a.srv_idle) {
+                  q = 0u;   // idle: exit (seq 0 is never issued)
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+              const uint64_t tsee = __builtin_amdgcn_s_memrealtime();
+              uint32_t op = 0u, n = 0u, fr = 0u, frel = 0u;
+              int64_t g0 = 0;
+              if (q) {
+                // (the field loads issue after the new seq came back: the
+                // host and the relay wrote the fields before seq, and the
+                // atomic loads read the coherence point, no fence needed)
+                if (relay) {
+                  op = __hip_atomic_load(&src->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  n = __hip_atomic_load(&src->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  g0 = __hip_atomic_load(&src->g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  fr = __hip_atomic_load(&src->fair, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  frel = __hip_atomic_load(&src->fair_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  // relay: the fields, then seq (release at agent scope)
+                  __hip_atomic_store(&mail->op, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(&mail->n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(&mail->g0, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(&mail->fair, fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(&mail->fair_rel, frel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  __hip_atomic_store(&mail->seq, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                  op = __hip_atomic_load(&src->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  n = __hip_atomic_load(&src->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  g0 = __hip_atomic_load(&src->g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  fr = __hip_atomic_load(&src->fair, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  frel = __hip_atomic_load(&src->fair_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+              }
+              s_cmd[0] = q;
+              s_cmd[1] = op;
+              s_cmd[2] = g0;
+              s_cmd[3] = n;
+              s_cmd[4] = ((int64_t)frel << 32) | fr;
+              s_cmd[5] = (int64_t)tsee;
+            }
+            __syncthreads();
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cmd[0]);
+            const uint32_t op = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_cmd[1]);
+            if (q == 0u || op == kSrvExit) {
+              if (poller && q != 0u)
+                __hip_atomic_store(&donep->seq, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+            const int64_t c2 = s_cmd[2], c4 = s_cmd[4];
+            g0v = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c2) |
+                  ((int64_t)__builtin_amdgcn_readfirstlane((int)(c2 >> 32)) << 32);
+            nsv = __builtin_amdgcn_readfirstlane((int)s_cmd[3]);
+            fairv = __builtin_amdgcn_readfirstlane((int)(uint32_t)c4);
+            fair_relv = __builtin_amdgcn_readfirstlane((int)(c4 >> 32));
+            const uint64_t tseen = (uint64_t)s_cmd[5];
+            __syncthreads();   // s_cmd read by every wave before the next poll
+            s = 0;
+            rec = g0v - a.rec_base;
+            run_block();
+            __builtin_amdgcn_s_waitcnt(0);   // this wave's stores have left
+            __syncthreads();
+            if (poller) {
+              __hip_atomic_store(&donep->t0, tseen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(&donep->t1, (uint64_t)__builtin_amdgcn_s_memrealtime(),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __builtin_amdgcn_s_waitcnt(0);   // the stamps before the seq
+              __hip_atomic_store(&donep->seq, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            seen = q;
+          }
+        } else {
+          run_block();
         }
         PBH_PHASE(3);
     } else {
@@ -3217,6 +3333,46 @@ void launch_mh_pair(const KArgs &a, hipStream_t st) {
   else launch_mh_pair_m<D, false>(a, st, grid, block);
 }
 
+// The resident server (engine pbh_server_*) runs the FULL lane-pair kernel
+// in 8-wave workgroups; each command must itself be a FULL launch.  check:
+// report whether `a` (with the command's g0 / n_steps) qualifies and whether
+// the whole grid fits the device at once (every workgroup resident: the
+// server's waves never wait for one another, but a workgroup that is not
+// resident would see no command until the others exit); otherwise launch.
+inline bool pair_form(const KArgs &a);
+template <int D>
+hipError_t launch_mh_server_d(const KArgs &a, hipStream_t st, int32_t *wgs, bool check) {
+  if constexpr (D % 2 == 0 && D >= 4) {
+    if (!(pair_form(a) && a.pair_ok && !a.moments && pair_full_form(a) &&
+          a.pair_wg == kPairFullBlock && a.srv_cmd && a.srv_done && a.srv_mail))
+      return hipErrorNotSupported;
+    const int64_t waves = a.n / 32;
+    const int64_t grid = (waves * 64 + kPairFullBlock - 1) / kPairFullBlock;
+    const void *kern = a.ploc_zero
+        ? reinterpret_cast<const void *>(mh_pair_kernel<D, PBH_RNG_PHILOX, false, true, true, true>)
+        : reinterpret_cast<const void *>(mh_pair_kernel<D, PBH_RNG_PHILOX, false, false, true, true>);
+    int dev = 0, cus = 0, per = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err == hipSuccess) err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err == hipSuccess)
+      err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kPairFullBlock, 0);
+    if (err != hipSuccess) return err;
+    if ((int64_t)per * cus < grid) return hipErrorNotSupported;
+    if (wgs) *wgs = (int32_t)grid;
+    if (check) return hipSuccess;
+    if (a.ploc_zero)
+      hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX, false, true, true, true>),
+                         dim3((unsigned)grid), dim3(kPairFullBlock), 0, st, a);
+    else
+      hipLaunchKernelGGL((mh_pair_kernel<D, PBH_RNG_PHILOX, false, false, true, true>),
+                         dim3((unsigned)grid), dim3(kPairFullBlock), 0, st, a);
+    return hipGetLastError();
+  } else {
+    (void)a; (void)st; (void)wgs; (void)check;
+    return hipErrorNotSupported;
+  }
+}
+
 // The lane-pair kernel covers the cfg2 form: diagonal Gaussian, callable
 // Gaussian delta, no ufun / prior, symmetric tran or metropolis, debug off.
 inline bool pair_form(const KArgs &a) {
@@ -3405,6 +3561,7 @@ hipError_t launch_gibbs_d(const KArgs &a, hipStream_t st) {
 
 #define PBH_INSTANTIATE(D)                                                  \
   template hipError_t launch_mh_d<D>(const KArgs &, hipStream_t, size_t); \
-  template hipError_t launch_gibbs_d<D>(const KArgs &, hipStream_t);
+  template hipError_t launch_gibbs_d<D>(const KArgs &, hipStream_t);      \
+  template hipError_t launch_mh_server_d<D>(const KArgs &, hipStream_t, int32_t *, bool);
 
 }  // namespace pbh

@@ -9,7 +9,9 @@ once per model, so the device sees bit-identical constants:
 Everything per chain-step runs in the HIP kernels; nothing here loops over
 chains or steps.
 """
+import atexit
 import ctypes
+import weakref
 
 import numpy as np
 import scipy.stats
@@ -78,6 +80,21 @@ def unpack_stats(out, counts, d):
           'counts': np.asarray(counts, np.int64)}
 
 
+# engines still open at interpreter exit are destroyed then (a resident
+# sampling server is stopped and its chain state stored: no kernel outlives
+# the process's last Python code)
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_engines():
+  for eng in list(_LIVE):
+    try:
+      eng.close()
+    except Exception:
+      pass
+
+
 class Engine:
   """One libpbhip engine on one device, running one lowered model."""
 
@@ -86,6 +103,7 @@ class Engine:
     self.dim = self.spec['dim']
     self._h = _c.c_void_p()
     _lib.call('pbh_create', int(device), _c.byref(self._h))
+    _LIVE.add(self)
     self.device = device
     self.n = 0
     self.chain_offset = 0
@@ -278,6 +296,30 @@ class Engine:
     ms, nl = _c.c_double(), _c.c_int64()
     _lib.call('pbh_last_run_ms', self._h, _c.byref(ms), _c.byref(nl))
     return ms.value, nl.value
+
+  def stop_server(self):
+    """Stops the resident sampling server (PBH_SERVER=1) if it runs: the
+    chain state is stored and the stream is idle afterwards."""
+    _lib.call('pbh_server_stop', self._h)
+
+  def server_stamps(self):
+    """Per-workgroup (seq, t0, t1) of the server's last command (10 ns)."""
+    cap = 4096
+    q = np.zeros(cap, np.uint32)
+    t0 = np.zeros(cap, np.uint64)
+    t1 = np.zeros(cap, np.uint64)
+    n = _c.c_int32()
+    _lib.call('pbh_server_stamps', self._h, cap, q.ctypes.data_as(_lib._u32p),
+              t0.ctypes.data_as(_lib._u64p), t1.ctypes.data_as(_lib._u64p),
+              _c.byref(n))
+    k = min(n.value, cap)
+    return q[:k], t0[:k], t1[:k]
+
+  def server_info(self):
+    """{'active', 'commands', 'launches'} of the resident sampling server."""
+    a, c, n = _c.c_int32(), _c.c_int64(), _c.c_int64()
+    _lib.call('pbh_server_info', self._h, _c.byref(a), _c.byref(c), _c.byref(n))
+    return {'active': bool(a.value), 'commands': c.value, 'launches': n.value}
 
   # ---- results -----------------------------------------------------------
   def state(self):
