@@ -236,6 +236,15 @@ int pbh_set_legacy_state(pbh_engine *eng, const uint32_t *key,
  * handed out.                                                               */
 int pbh_set_chains(pbh_engine *eng, const double *x, const double *lp,
                    int64_t step, int32_t has_pred);
+/* The carried logs of the ufun dims (production modes: the log of a ufun
+ * dim is chain state, the accepted proposal's log x + delta, variable.py:
+ * 693-697 without the round trip through exp): lx [N][d] row-major (the
+ * non-ufun columns unused); valid = 0 when they are not maintained (another
+ * RNG mode, or a fresh / restored state: then ln x at the next launch).  A
+ * checkpoint of a production ufun model carries them so that a restored
+ * engine continues the run bit for bit.                                    */
+int pbh_get_chain_logs(pbh_engine *eng, double *lx, int32_t *valid);
+int pbh_set_chain_logs(pbh_engine *eng, const double *lx);
 /* Replay stream [n_steps][R][n_chains] (R = d + 1 for MH, 1 for Gibbs),
  * consumed from the next pbh_run step on.                                   */
 int pbh_upload_replay(pbh_engine *eng, int64_t n_steps, const double *rand);

@@ -97,6 +97,8 @@ SIGNATURES = {
     'pbh_set_collect': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     'pbh_last_run_ms': (ctypes.c_int, [ctypes.c_void_p, _dp, _i64p]),
     'pbh_server_stop': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_get_chain_logs': (ctypes.c_int, [ctypes.c_void_p, _dp, _ip]),
+    'pbh_set_chain_logs': (ctypes.c_int, [ctypes.c_void_p, _dp]),
     'pbh_server_info': (ctypes.c_int, [ctypes.c_void_p, _ip, _i64p, _i64p]),
     'pbh_server_stamps': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _u32p,
                                          _u64p, _u64p, _ip]),

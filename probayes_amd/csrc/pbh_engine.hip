@@ -111,6 +111,9 @@ struct pbh_engine {
   double mvn_const = 0.;
   // production Gibbs: persisted g = P'(x - mu'), Q per chain
   double *gq = nullptr;
+  // production ufun logs carried as chain state ([d][n], KArgs.lx)
+  double *lx = nullptr;
+  bool lx_valid = false;
   bool gq_valid = false;
   // timing of the last pbh_run
   bool timed = false;
@@ -434,7 +437,7 @@ int pbh_destroy(pbh_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
-  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq);
+  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq); dfree(e->lx);
   dfree(e->mt_key); dfree(e->mt_pos); dfree(e->mt_has); dfree(e->mt_order);
   dfree(e->mt_gauss);
   free_trace(e);
@@ -599,6 +602,7 @@ int pbh_set_model(pbh_engine *e, const pbh_model *m) {
   }
   e->d = d;
   e->has_model = true;
+  e->lx_valid = false;   // the ufun mask may differ
   return PBH_OK;
 }
 
@@ -800,6 +804,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
     if (!rc) rc = dalloc(e->nacc, n);
     if (!rc) rc = dalloc(e->xo, (size_t)8 * n);
     if (!rc) rc = dalloc(e->gq, (size_t)(d + 1) * n);
+    if (!rc) rc = dalloc(e->lx, (size_t)d * n);
     if (!rc) rc = dalloc(e->ess, (size_t)d * n);
     if (rc) return rc;
   }
@@ -809,6 +814,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
                       hipMemcpyHostToDevice));
   }
   e->gq_valid = false;
+  e->lx_valid = false;
   std::vector<double> xt((size_t)n * d);
   for (int64_t c = 0; c < n; ++c)
     for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = init[(size_t)c * d + k];
@@ -1292,6 +1298,8 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     k.has_pred = e->has_pred ? 1 : 0;
     k.rep_row0 = e->g - e->rep_g0;
     k.gq_init = e->gq_valid ? 0 : 1;
+    k.lx = e->lx;
+    k.lx_init = e->lx_valid ? 0 : 1;
     hipError_t err = e->has_gibbs ? pbh::launch_gibbs(k, e->stream)
                                   : pbh::launch_mh(k, e->stream, lds);
     if (err != hipSuccess) {
@@ -1301,6 +1309,9 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     e->g += m;
     e->has_pred = true;
     e->gq_valid = gfast;   // only the production Gibbs kernel maintains g, Q
+    // the production MH kernels maintain the carried ufun logs
+    e->lx_valid = !e->has_gibbs && k.ufun != 0 &&
+                  (e->rng == PBH_RNG_PHILOX || e->rng == PBH_RNG_XOSHIRO);
     done += m;
     ++launches;
   }
@@ -1487,6 +1498,7 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
   e->g = step;
   e->has_pred = has_pred != 0;
   e->gq_valid = false;   // the production Gibbs kernel recomputes g, Q from x
+  e->lx_valid = false;   // ... and the ufun logs (pbh_set_chain_logs restores them)
   e->cap = 0;            // a trace / replay rows of the engine are detached
   e->rep_steps = 0;
   e->rep_g0 = step;
@@ -1515,9 +1527,41 @@ int pbh_set_chains(pbh_engine *e, const double *x, const double *lp,
   e->g = step;
   e->has_pred = has_pred != 0;
   e->gq_valid = false;
+  e->lx_valid = false;
   e->cap = 0;            // the trace and the replay rows are detached
   e->rep_steps = 0;
   e->rep_g0 = step;
+  return PBH_OK;
+}
+
+int pbh_get_chain_logs(pbh_engine *e, double *lx, int32_t *valid) {
+  if (check_ptr(e, "engine") || check_ptr(valid, "valid")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  *valid = e->lx_valid ? 1 : 0;
+  if (!e->lx_valid || !lx) return PBH_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const int64_t n = e->n, d = e->d;
+  std::vector<double> t((size_t)n * d);
+  HIP_TRY(hipMemcpy(t.data(), e->lx, t.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (int64_t c = 0; c < n; ++c)
+    for (int64_t k = 0; k < d; ++k) lx[(size_t)c * d + k] = t[(size_t)k * n + c];
+  return PBH_OK;
+}
+
+int pbh_set_chain_logs(pbh_engine *e, const double *lx) {
+  if (check_ptr(e, "engine") || check_ptr(lx, "lx")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const int64_t n = e->n, d = e->d;
+  std::vector<double> t((size_t)n * d);
+  for (int64_t c = 0; c < n; ++c)
+    for (int64_t k = 0; k < d; ++k) t[(size_t)k * n + c] = lx[(size_t)c * d + k];
+  HIP_TRY(hipMemcpy(e->lx, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+  e->lx_valid = true;
   return PBH_OK;
 }
 

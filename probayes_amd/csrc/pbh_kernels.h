@@ -115,6 +115,12 @@ struct KArgs {
   double gconst;       // rank * log(2 pi) + log_pdet
   double *gq;          // persisted g = P'(x - mu') [d][n] and Q [n]
   int32_t gq_init;     // 1: recompute g, Q from x at entry
+  // production modes (PHILOX, XOSHIRO) with ufun dims: the log of each ufun
+  // dim of the state is chain state, [d][N], carried from the accepted
+  // proposal's log (x' = exp(lx + delta), lx' = lx + delta) instead of the
+  // log of the exp'd value at every step; lx_init = 1: ln x at entry
+  double *lx;
+  int32_t lx_init;
   int32_t gibbs_lanes; // lanes per chain (1, 2, 4; 0 = default for d)
   int32_t gmm_lanes;   // lanes per chain of the GMM kernel (2 or 4)
   int32_t gmm_full;    // the quad kernel's steady-state form is allowed

@@ -479,6 +479,14 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   const int64_t chain = a.off + cc;
   Xo xs{0u, 0u, 0u, 0u};
   if (RNG == PBH_RNG_XOSHIRO) xs = xo_load(a, 0, cc);
+  // production: the carried logs of the ufun dims (KArgs.lx)
+  double lx[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    lx[k] = 0.;
+    if (FAST && ((a.ufun >> k) & 1u))
+      lx[k] = a.lx_init ? ln_ufun(x[k], s_bmt) : a.lx[k * a.n + cc];
+  }
 
   // record phase / index of the trace, advanced per step (no 64-bit
   // division in the loop): step g records iff (g + 1) % thin == 0, at
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
       for (int k = 0; k < D; ++k) {
         if ((a.ufun >> k) & 1u) {
           if (FAST) {
-            lxp[k] = ln_ufun(x[k], s_bmt) + dl[k];
+            lxp[k] = lx[k] + dl[k];
             xp[k] = exp_ufun(lxp[k], s_bmt);
           } else {
             xp[k] = exp(log(x[k]) + dl[k]);
@@ -698,7 +706,10 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     }
     if (acc) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) x[k] = xp[k];
+      for (int k = 0; k < D; ++k) {
+        x[k] = xp[k];
+        if (FAST) lx[k] = lxp[k];
+      }
       lp = lpp;
       eB = eA;
     }
@@ -737,7 +748,10 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
 
   if (active) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
+    for (int k = 0; k < D; ++k) {
+      a.x[k * a.n + c] = x[k];
+      if (FAST && ((a.ufun >> k) & 1u)) a.lx[k * a.n + c] = lx[k];
+    }
     a.lp[c] = lp;
     if (mom) {
 #pragma unroll
@@ -779,6 +793,10 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
 #pragma unroll
   for (int k = 0; k < D; ++k) plen[k] = cld(a.plen, k);
   bm64_load(s_bmt, a.bm64);
+  double lx[D];   // the carried logs of the ufun dims (KArgs.lx)
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    lx[k] = ((UFM >> k) & 1) ? (a.lx_init ? ln_ufun(x[k], s_bmt) : a.lx[k * a.n + cc]) : 0.;
   __builtin_amdgcn_s_waitcnt(0);
   const double d0 = a.sdelta;
   const double beta = a.acc_beta;
@@ -842,7 +860,7 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
       dl[k] = (dl[k] * sc) * plen[k];
       lxp[k] = 0.;
       if (((UFM >> k) & 1) != 0) {   // folded per unrolled k
-        lxp[k] = ln_ufun(x[k], s_bmt) + dl[k];
+        lxp[k] = lx[k] + dl[k];
         xp[k] = exp_ufun(lxp[k], s_bmt);
       } else {
         xp[k] = x[k] + dl[k];
@@ -891,7 +909,10 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
       accm = (accm & ~needm) | (__ballot(ex) & needm);
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = sel_f64(accm, x[k], xp[k]);
+    for (int k = 0; k < D; ++k) {
+      x[k] = sel_f64(accm, x[k], xp[k]);
+      if ((UFM >> k) & 1) lx[k] = sel_f64(accm, lx[k], lxp[k]);
+    }
     lp = sel_f64(accm, lp, lpp);
     // ---- trace: record g - rec_base = r0 + s ----
 #pragma unroll
@@ -902,7 +923,10 @@ __global__ __launch_bounds__(kBlock) void mh_iid_full_kernel(KArgs a) {
   }
   if (active) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
+    for (int k = 0; k < D; ++k) {
+      a.x[k * a.n + c] = x[k];
+      if ((UFM >> k) & 1) a.lx[k * a.n + c] = lx[k];
+    }
     a.lp[c] = lp;
   }
 }
@@ -974,9 +998,8 @@ __device__ __forceinline__ void rowpair_f64(double v, double &ev, double &od) {
 // v_permlane32_swap exchanges per double give both halves both steps'.
 // Both halves then run the state update (ufun, density, filter, selects) on
 // identical values, so every lane holds the chain's state.  The log of a
-// ufun dim of the state is carried: ln x' of the proposal is evaluated beside
-// the density and the decision instead of ln x at the next step's head (the
-// same function of the same value: the same bits).  Half 0 stores dim 0 and
+// ufun dim of the state is chain state (KArgs.lx, as in every production
+// kernel): the accepted proposal's lx + delta.  Half 0 stores dim 0 and
 // the lp row, half 1 dim 1 (D = 2: one store instruction for both dims), and
 // each wavefront writes its 32-bit half of the record's 64-bit accept word.
 // The draws and arithmetic are mh_iid_full_kernel's: identical chains
@@ -1020,7 +1043,8 @@ void mh_iid_pair_kernel(KArgs a) {
   }
   double lx[D];   // ln x of the ufun dims of the state
 #pragma unroll
-  for (int k = 0; k < D; ++k) lx[k] = ((UFM >> k) & 1) ? ln_ufun(x[k], s_bmt) : 0.;
+  for (int k = 0; k < D; ++k)
+    lx[k] = ((UFM >> k) & 1) ? (a.lx_init ? ln_ufun(x[k], s_bmt) : a.lx[k * a.n + cc]) : 0.;
   const uint32_t rowb = (uint32_t)(a.n * 8);
   // stores: half 0 dim 0 + lp, half 1 dim 1 (a D = 1 chain: half 0 only)
   const uint32_t xoff = active && (D == 2 || h == 0) ? (uint32_t)(h * a.n * 8 + c * 8) : kNoStore;
@@ -1087,9 +1111,6 @@ void mh_iid_pair_kernel(KArgs a) {
       }
       // the proposal's ln x' (the next state's, if accepted): beside the
       // density and the decision
-      double lnp[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) lnp[k] = ((UFM >> k) & 1) ? ln_ufun(xp[k], s_bmt) : 0.;
       // joint_density<D, NORM_IID, FAST> (mh_iid_full_kernel's operations)
       double lpp;
       {
@@ -1132,7 +1153,7 @@ void mh_iid_pair_kernel(KArgs a) {
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         x[k] = sel_f64(accm, x[k], xp[k]);
-        if ((UFM >> k) & 1) lx[k] = sel_f64(accm, lx[k], lnp[k]);
+        if ((UFM >> k) & 1) lx[k] = sel_f64(accm, lx[k], lxp[k]);
       }
       lp = sel_f64(accm, lp, lpp);
       // ---- trace: record g - rec_base ----
@@ -1146,7 +1167,10 @@ void mh_iid_pair_kernel(KArgs a) {
   }
   if (active && h == 0) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.x[k * a.n + c] = x[k];
+    for (int k = 0; k < D; ++k) {
+      a.x[k * a.n + c] = x[k];
+      if ((UFM >> k) & 1) a.lx[k * a.n + c] = lx[k];
+    }
     a.lp[c] = lp;
   }
 }

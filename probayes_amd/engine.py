@@ -339,8 +339,12 @@ class Engine:
     _lib.call('pbh_get_checkpoint', self._h, _dp(x), _dp(lp), _c.byref(step),
               _c.byref(hp),
               None if xo is None else xo.ctypes.data_as(_lib._u32p))
+    lx = np.empty((self.n, self.dim))
+    valid = _c.c_int32()
+    _lib.call('pbh_get_chain_logs', self._h, _dp(lx), _c.byref(valid))
     return {'x': x, 'lp': lp, 'step': step.value, 'has_pred': bool(hp.value),
-            'xo': xo, 'mt': self._legacy_state(), 'chain_offset': self.chain_offset}
+            'xo': xo, 'mt': self._legacy_state(), 'chain_offset': self.chain_offset,
+            'lx': lx if valid.value else None}
 
   def _legacy_state(self):
     """The device legacy streams' state (key, pos, has, gauss) or None."""
@@ -406,6 +410,13 @@ class Engine:
     _lib.call('pbh_restore', self._h, _dp(x), _dp(lp),
               _c.c_int64(int(ck['step'])), 1 if ck['has_pred'] else 0,
               None if xo is None else xo.ctypes.data_as(_lib._u32p))
+    lx = ck.get('lx')
+    if lx is not None:   # the production ufun logs (pbh_set_chain_logs)
+      lx = np.ascontiguousarray(lx, np.float64)
+      if lx.shape != (self.n, self.dim):
+        raise ValueError('checkpoint ufun logs have shape {}, the engine needs {}'
+                         .format(lx.shape, (self.n, self.dim)))
+      _lib.call('pbh_set_chain_logs', self._h, _dp(lx))
     if mt is not None:   # device legacy streams continue where they were
       key = np.ascontiguousarray(mt['key'], np.uint32)
       pos = np.ascontiguousarray(mt['pos'], np.int32)

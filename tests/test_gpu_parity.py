@@ -644,6 +644,9 @@ def test_extreme_dims_and_chain_counts_replay(d, n):
 
 @pytest.mark.parametrize('name,rng', [('diag10', 'philox'), ('gmm2', 'philox'),
                                       ('metrohast_norm1d', 'philox_f64'),
+                                      # production ufun: the carried logs
+                                      ('metrohast_norm1d', 'philox'),
+                                      ('metrohast_norm1d', 'xoshiro'),
                                       ('diag10', 'xoshiro'),
                                       ('gibbs8', 'philox')])
 def test_checkpoint_resume_continues_the_run(name, rng):
