@@ -197,10 +197,21 @@ def kernel_label(args, n):
 
 
 class EngineCollective:
-  """The engine's own RCCL collectives (pbh_rccl_*): the production path."""
+  """The engine's own RCCL collectives (pbh_rccl_*): the production path.
+  host: a dist.TcpCollective for the barriers around the timed region (an
+  RCCL call stops the resident server -- its kernel holds the device -- so
+  the barrier before t0 is a host barrier; the max-over-ranks time and the
+  statistics gather after it stay RCCL)."""
 
-  def __init__(self, eng):
+  def __init__(self, eng, host=None):
     self.eng = eng
+    self.host = host
+
+  def barrier(self):
+    if self.host is not None:
+      self.host.allreduce_max(0.0)
+    else:
+      self.eng.rccl_allreduce_max(0.0)
 
   def allreduce_max(self, v):
     return self.eng.rccl_allreduce_max(v)
@@ -228,7 +239,10 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
   def barrier():
     eng.sync()
     if col is not None:
-      col.allreduce_max(0.0)
+      if hasattr(col, 'barrier'):
+        col.barrier()
+      else:
+        col.allreduce_max(0.0)
 
   if warmup and warmup_spl is None and warmup <= 16:
     # a short warm-up runs as one-step runs, one pbh_run call each, so that
@@ -294,7 +308,10 @@ def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup
   def barrier():
     eng.sync()
     if col is not None:
-      col.allreduce_max(0.0)
+      if hasattr(col, 'barrier'):
+        col.barrier()
+      else:
+        col.allreduce_max(0.0)
 
   if warmup:
     advance(warmup)
@@ -369,7 +386,8 @@ def main():
                              Engine.rccl_unique_id() if rank == 0 else None,
                              addr, port)
     eng.rccl_init(rank, world, uid)
-    col = EngineCollective(eng)
+    from probayes_amd.dist import TcpCollective
+    col = EngineCollective(eng, TcpCollective(rank, world, addr, port + 1))
   spl = args.steps_per_launch
   res = run_rank(eng, col, rank, world, args.chains, args.steps, args.warmup,
                  spl, args.rng, trace=not args.no_trace, moments=args.moments,
@@ -446,6 +464,8 @@ def main():
     if cpu is not None:
       line['cpu_baseline'] = cpu
     print(json.dumps(line), flush=True)
+  if col is not None and getattr(col, 'host', None) is not None:
+    col.host.close()
   eng.close()
 
 

@@ -300,7 +300,7 @@ class MainEngine(OracleEngine):
   def rccl_init(self, rank_, world_, uid):
     assert uid == bytes(range(128)) and self.device == rank_
     self.col = TcpCollective(rank_, world_, '127.0.0.1',
-                             int(os.environ['MASTER_PORT']) + 2)
+                             int(os.environ['MASTER_PORT']) + 3)
   def rccl_allreduce_max(self, v):
     return self.col.allreduce_max(v)
   def rccl_allgather_stats(self):
