@@ -270,7 +270,8 @@ int srv_stop(pbh_engine *e) {
   }
   if (!srv_kernel_ended(e)) {
     const uint32_t q = ++e->srv_seq;
-    e->srv_cmd->op = pbh::kSrvExit;
+    e->srv_cmd->n = 0u;
+    e->srv_cmd->arg = pbh::srv_arg(0, 0u, 0u, pbh::kSrvExit, q);
     __atomic_store_n(&e->srv_cmd->seq, q, __ATOMIC_RELEASE);
     const int rc2 = srv_wait(e, q, true);
     if (!rc) rc = rc2;
@@ -1223,10 +1224,11 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     // a running server's form (model, proposal, RNG, trace) was checked at
     // its launch -- every entry point that changes them stops it -- so only
     // this run's own shape is checked (no occupancy query per command)
-    const bool form = e->srv_active
-        ? (!k.moments && e->has_pred && e->cap > 0 && e->thin == 1 &&
-           e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap)
-        : pbh::launch_mh_server(kc, e->stream, &wgs, true) == hipSuccess;
+    const bool form = e->g + n_steps < (int64_t(1) << 47) &&   // srv_arg's 48-bit step
+        (e->srv_active
+             ? (!k.moments && e->has_pred && e->cap > 0 && e->thin == 1 &&
+                e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap)
+             : pbh::launch_mh_server(kc, e->stream, &wgs, true) == hipSuccess);
     if (form) {
       if (e->srv_active) {
         if (e->srv_pending) {   // one command in flight
@@ -1251,13 +1253,10 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
         if (rc) return rc;
       }
       pbh::SrvCmd *cmd = e->srv_cmd;
-      cmd->op = pbh::kSrvRun;
-      cmd->g0 = e->g;
-      cmd->n = (int32_t)n_steps;
-      cmd->fair = kc.fair;
-      cmd->fair_rel = kc.fair_rel;
       const uint32_t q = ++e->srv_seq;
-      __atomic_store_n(&cmd->seq, q, __ATOMIC_RELEASE);
+      cmd->n = (uint32_t)n_steps;
+      cmd->arg = pbh::srv_arg(e->g, (uint32_t)kc.fair, (uint32_t)kc.fair_rel, pbh::kSrvRun, q);
+      __atomic_store_n(&cmd->seq, q, __ATOMIC_RELEASE);   // n and arg first
       e->srv_pending = q;
       e->srv_last = srv_clk::now();
       e->g += n_steps;

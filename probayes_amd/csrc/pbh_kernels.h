@@ -152,11 +152,20 @@ struct KArgs {
 // of the same layout, which every other workgroup's first wave polls; each
 // workgroup runs the command and writes its SrvDone (seq last) to host
 // memory.  op: 0 run, 1 exit.
-struct SrvCmd {
+// One 16-byte record, read and relayed whole (one PCIe read, one mailbox
+// store): seq, n, then arg = g0 (bits 0-47) | fair (48-52) | fair_rel (53)
+// | op (54) | seq & 0xFF (56-63).  The check byte rejects a torn read (new
+// seq, old fields): the host writes n and arg, then seq.
+struct alignas(16) SrvCmd {
   uint32_t seq, n;
-  int64_t g0;
-  uint32_t op, fair, fair_rel, pad;
+  uint64_t arg;
 };
+__host__ __device__ inline uint64_t srv_arg(int64_t g0, uint32_t fair, uint32_t fair_rel,
+                                            uint32_t op, uint32_t seq) {
+  return ((uint64_t)g0 & 0xFFFFFFFFFFFFull) | ((uint64_t)(fair & 31u) << 48) |
+         ((uint64_t)(fair_rel & 1u) << 53) | ((uint64_t)(op & 1u) << 54) |
+         ((uint64_t)(seq & 0xFFu) << 56);
+}
 struct SrvDone {
   uint32_t seq, pad;
   uint64_t t0, t1;   // s_memrealtime (100 MHz) when the command was seen / done

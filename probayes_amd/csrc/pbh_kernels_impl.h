@@ -1302,6 +1302,20 @@ struct PairDraw {
 // decide): t's remaining 53 - 16 bits from a block of this step alone and
 // the exact fp64 ratio form, out of line (the loop keeps neither its
 // registers nor its code).
+// The resident server's 16-byte command record, read and written whole with
+// caches bypassed (sc0 sc1: host memory over PCIe, and the device mailbox at
+// the coherence point, past the XCD's own L2).  The load waits for itself.
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4v ld16_sys(const void *p) {
+  u32x4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void st16_sys(void *p, u32x4v v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
 __device__ __attribute__((noinline)) bool pair_exact(uint32_t seed_lo, uint32_t seed_hi,
                                                      double log_npi, int64_t g,
                                                      int64_t chain, int h,
@@ -1781,16 +1795,16 @@ void mh_pair_kernel(KArgs a) {
           for (;;) {
             if (poller) {
               const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-              // workgroup 0 reads the host block (system scope, uncached);
-              // the others the device mailbox (agent scope)
-              SrvCmd *const src = relay ? hcmd : mail;
+              // workgroup 0 reads the host block, the others the device
+              // mailbox: one 16-byte volatile load (caches bypassed) per poll
+              const SrvCmd *src = relay ? hcmd : mail;
               uint32_t q;
+              u32x4v v;
               for (;;) {
-                q = relay ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
-                                &src->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
-                          : (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
-                                &src->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                if (q != seen) break;
+                v = ld16_sys(src);
+                q = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
+                const uint32_t chk = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w) >> 24;
+                if (q != seen && chk == (q & 0xFFu)) break;   // new and whole
                 if (__builtin_amdgcn_s_memrealtime() - tw > (uint64_t)a.srv_idle) {
                   q = 0u;   // idle: exit (seq 0 is never issued)
                   break;
@@ -1798,33 +1812,14 @@ void mh_pair_kernel(KArgs a) {
                 __builtin_amdgcn_s_sleep(1);
               }
               const uint64_t tsee = __builtin_amdgcn_s_memrealtime();
-              uint32_t op = 0u, n = 0u, fr = 0u, frel = 0u;
-              int64_t g0 = 0;
-              if (q) {
-                // (the field loads issue after the new seq came back: the
-                // host and the relay wrote the fields before seq, and the
-                // atomic loads read the coherence point, no fence needed)
-                if (relay) {
-                  op = __hip_atomic_load(&src->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  n = __hip_atomic_load(&src->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  g0 = __hip_atomic_load(&src->g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  fr = __hip_atomic_load(&src->fair, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  frel = __hip_atomic_load(&src->fair_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                  // relay: the fields, then seq (release at agent scope)
-                  __hip_atomic_store(&mail->op, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  __hip_atomic_store(&mail->n, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  __hip_atomic_store(&mail->g0, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  __hip_atomic_store(&mail->fair, fr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  __hip_atomic_store(&mail->fair_rel, frel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  __hip_atomic_store(&mail->seq, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                  op = __hip_atomic_load(&src->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  n = __hip_atomic_load(&src->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  g0 = __hip_atomic_load(&src->g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  fr = __hip_atomic_load(&src->fair, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  frel = __hip_atomic_load(&src->fair_rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-              }
+              if (relay && q) st16_sys(mail, v);   // relay, whole
+              const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.y);
+              const uint64_t arg =
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.z) |
+                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v.w) << 32);
+              const int64_t g0 = (int64_t)(arg & 0xFFFFFFFFFFFFull);
+              const uint32_t fr = (uint32_t)(arg >> 48) & 31u, frel = (uint32_t)(arg >> 53) & 1u;
+              const uint32_t op = (uint32_t)(arg >> 54) & 1u;
               s_cmd[0] = q;
               s_cmd[1] = op;
               s_cmd[2] = g0;
@@ -1847,7 +1842,8 @@ void mh_pair_kernel(KArgs a) {
             fairv = __builtin_amdgcn_readfirstlane((int)(uint32_t)c4);
             fair_relv = __builtin_amdgcn_readfirstlane((int)(c4 >> 32));
             const uint64_t tseen = (uint64_t)s_cmd[5];
-            __syncthreads();   // s_cmd read by every wave before the next poll
+            // (the poller writes s_cmd again only after the command's closing
+            // barrier: every wave has read it by then)
             s = 0;
             rec = g0v - a.rec_base;
             run_block();
