@@ -296,6 +296,9 @@ def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup
   eng.seed_legacy(offset + np.arange(n))
   eng.alloc_trace(warmup + steps, 1)
   chunk = max(1, min(spl, steps))
+  # the stream buffer sized once for the largest generation (a growth inside
+  # the timed region would be a 100 MB-class hipMalloc there)
+  eng.reserve_replay(max(chunk, min(spl, warmup) if warmup else 1))
 
   def advance(k):
     done = 0

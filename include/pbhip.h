@@ -260,6 +260,11 @@ int pbh_stream_width(pbh_engine *eng, int32_t *r);
  * the pbh_upload_replay layout [n][R][N], draw = j only draw j, [n][N].   */
 int pbh_legacy_seed(pbh_engine *eng, const uint32_t *seeds);
 int pbh_legacy_replay(pbh_engine *eng, int64_t n_steps);
+/* Sizes the replay stream buffer for n_steps rows without drawing (the
+ * buffer only grows; a later generation or upload of at most that many rows
+ * allocates nothing).  Rows already in the buffer are dropped when it grows:
+ * reserve before filling it.                                               */
+int pbh_reserve_replay(pbh_engine *eng, int64_t n_steps);
 int pbh_get_replay(pbh_engine *eng, int64_t first, int64_t n_steps,
                    int32_t draw, double *out);
 

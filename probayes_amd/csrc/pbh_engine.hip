@@ -934,6 +934,26 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
   return PBH_OK;
 }
 
+int pbh_reserve_replay(pbh_engine *e, int64_t n_steps) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  int32_t R = 0;
+  int rc = pbh_stream_width(e, &R);
+  if (rc) return rc;
+  if (n_steps < 1) return fail(PBH_ERR_ARG, "n_steps must be >= 1");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  const size_t need = (size_t)n_steps * R * e->n;
+  if (!e->rep || e->rep_alloc < need) {
+    // the stream rows in use (if any) are not kept: reserve before the
+    // generation or upload that fills them
+    rc = dalloc(e->rep, need);
+    e->rep_alloc = rc ? 0 : need;
+    e->rep_steps = 0;
+  }
+  return rc;
+}
+
 int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   SRV_STOP(e);

@@ -262,6 +262,12 @@ class Engine:
     device RandomState (the reference's per-step draw order)."""
     _lib.call('pbh_legacy_replay', self._h, _c.c_int64(int(n_steps)))
 
+  def reserve_replay(self, n_steps):
+    """Sizes the replay stream buffer for n_steps rows (draws nothing): a
+    later legacy_replay / upload_replay of at most that many rows allocates
+    nothing.  Call it before filling the buffer."""
+    _lib.call('pbh_reserve_replay', self._h, _c.c_int64(int(n_steps)))
+
   def get_replay(self, first, n_steps, draw=-1):
     """Rows of the current replay stream: [n, R, N], or [n, N] of one draw."""
     r = self.stream_width()

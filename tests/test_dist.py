@@ -311,6 +311,8 @@ class MainEngine(OracleEngine):
     assert len(seeds) == len(self.x0) and seeds[0] == self.off
   def legacy_replay(self, k):
     assert k >= 1
+  def reserve_replay(self, k):
+    assert k >= 1
   def close(self):
     if getattr(self, 'col', None) is not None:
       self.col.close()
