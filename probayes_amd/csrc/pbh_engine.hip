@@ -334,6 +334,23 @@ int srv_launch(pbh_engine *e, pbh::KArgs k) {
   ++e->srv_launches;
   return PBH_OK;
 }
+// a run command (the previous one completed): n and arg, then seq
+void srv_submit(pbh_engine *e, int64_t n_steps, int32_t fair, int32_t fair_rel) {
+  pbh::SrvCmd *cmd = e->srv_cmd;
+  const uint32_t q = ++e->srv_seq;
+  cmd->n = (uint32_t)n_steps;
+  cmd->arg = pbh::srv_arg(e->g, (uint32_t)fair, (uint32_t)fair_rel, pbh::kSrvRun, q);
+  __atomic_store_n(&cmd->seq, q, __ATOMIC_RELEASE);
+  e->srv_pending = q;
+  e->srv_last = srv_clk::now();
+  e->g += n_steps;
+  e->has_pred = true;
+  e->mom_steps += n_steps;
+  e->timed = true;
+  e->srv_timed = true;
+  e->last_launches = 1;
+  ++e->srv_commands;
+}
 }  // namespace
 
 #define SRV_STOP(e)                        \
@@ -1168,6 +1185,27 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
       return fail(PBH_ERR_STATE, "trace capacity %lld < %lld records",
                   (long long)e->cap, (long long)recs);
   }
+  // a running server and a run of its form: the command straight away (no
+  // kernel-argument block, no device call; the server's form was checked at
+  // its launch and every entry point that could change it stops it)
+  if (e->srv_active && (steps_per_launch <= 0 || steps_per_launch >= n_steps) &&
+      n_steps <= (1 << 30) && e->g + n_steps < (int64_t(1) << 47) &&
+      !(e->collect & PBH_COLLECT_MOMENTS) && e->has_pred && e->cap > 0 && e->thin == 1 &&
+      e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap) {
+    if (e->srv_pending) {
+      const int rc = srv_wait(e, e->srv_pending, false);
+      e->srv_pending = 0;
+      e->srv_last = srv_clk::now();
+      if (rc) return rc;
+    }
+    if (srv_clk::now() - e->srv_last <= std::chrono::milliseconds(e->srv_idle_ms / 2)) {
+      const bool short_run = n_steps <= 64;
+      srv_submit(e, n_steps, short_run ? e->fair_short : e->fair,
+                 short_run ? 1 : e->fair_rel);
+      tq("server command (fast path)");
+      return PBH_OK;
+    }
+  }
   HIP_TRY(hipSetDevice(e->device));
   if (e->rng == PBH_RNG_XOSHIRO && !e->xo_seeded) {
     HIP_TRY(pbh::launch_xo_seed(e->xo, e->n, e->off, e->seed, e->stream));
@@ -1272,20 +1310,7 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
         const int rc = srv_launch(e, kc);
         if (rc) return rc;
       }
-      pbh::SrvCmd *cmd = e->srv_cmd;
-      const uint32_t q = ++e->srv_seq;
-      cmd->n = (uint32_t)n_steps;
-      cmd->arg = pbh::srv_arg(e->g, (uint32_t)kc.fair, (uint32_t)kc.fair_rel, pbh::kSrvRun, q);
-      __atomic_store_n(&cmd->seq, q, __ATOMIC_RELEASE);   // n and arg first
-      e->srv_pending = q;
-      e->srv_last = srv_clk::now();
-      e->g += n_steps;
-      e->has_pred = true;
-      e->mom_steps += n_steps;
-      e->timed = true;
-      e->srv_timed = true;
-      e->last_launches = 1;
-      ++e->srv_commands;
+      srv_submit(e, n_steps, kc.fair, kc.fair_rel);
       tq("server command");
       return PBH_OK;
     }
