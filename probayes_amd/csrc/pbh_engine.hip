@@ -237,24 +237,34 @@ using srv_clk = std::chrono::steady_clock;
 
 bool srv_kernel_ended(pbh_engine *e) { return hipStreamQuery(e->stream) == hipSuccess; }
 
+// the first workgroup from `from` on that has not reported `seq` (srv_wgs:
+// all have)
+int32_t srv_first_pending(const pbh_engine *e, uint32_t seq, int32_t from) {
+  for (int32_t w = from; w < e->srv_wgs; ++w)
+    if (__atomic_load_n(&e->srv_done[w].seq, __ATOMIC_ACQUIRE) != seq) return w;
+  return e->srv_wgs;
+}
 bool srv_all_done(const pbh_engine *e, uint32_t seq) {
-  for (int32_t w = 0; w < e->srv_wgs; ++w)
-    if (__atomic_load_n(&e->srv_done[w].seq, __ATOMIC_ACQUIRE) != seq) return false;
-  return true;
+  return srv_first_pending(e, seq, 0) == e->srv_wgs;
 }
 
 // every workgroup reported `seq`; ok_if_ended: an ended kernel is no error
-// (the exit command: workgroups that left idle do not acknowledge it)
+// (the exit command: workgroups that left idle do not acknowledge it).  The
+// scan resumes at the first workgroup not yet seen done; the stream is
+// queried (a runtime call with a lock) only after a millisecond of waiting.
 int srv_wait(pbh_engine *e, uint32_t seq, bool ok_if_ended) {
   const auto t0 = srv_clk::now();
+  int32_t w = 0;
   for (uint64_t it = 1;; ++it) {
-    if (srv_all_done(e, seq)) return PBH_OK;
-    if ((it & 1023) == 0) {
-      if (srv_kernel_ended(e)) {
+    w = srv_first_pending(e, seq, w);
+    if (w == e->srv_wgs) return PBH_OK;
+    if ((it & 4095) == 0) {
+      const auto el = srv_clk::now() - t0;
+      if (el > std::chrono::milliseconds(1) && srv_kernel_ended(e)) {
         if (srv_all_done(e, seq) || ok_if_ended) return PBH_OK;
         return fail(PBH_ERR_HIP, "sampling server ended before command %u completed", seq);
       }
-      if (srv_clk::now() - t0 > std::chrono::seconds(120))
+      if (el > std::chrono::seconds(120))
         return fail(PBH_ERR_HIP, "sampling server: command %u not completed in 120 s", seq);
     }
   }
