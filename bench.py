@@ -282,12 +282,15 @@ def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup
                     spl):
   """The parity-carrying mode on the same cfg2 shape:
   REPLAY -- the kernels read one NumPy RandomState(global chain id) stream
-  per chain, generated on the device (pbh_legacy_seed / pbh_legacy_replay:
-  MT19937 + the polar legacy gauss, the reference's per-step draw order), and
-  run the reference's arithmetic, so chains equal the reference CPU path's.
-  Timed like the headline (barrier + sync on both sides, max over ranks):
-  stream generation and the replay launches of exactly `steps` steps, the
-  full trace written.  Returns chain-steps/s of the whole job (not `value`)."""
+  per chain, generated on the device (pbh_legacy_seed; MT19937 + the polar
+  legacy gauss, the reference's per-step draw order), and run the
+  reference's arithmetic, so chains equal the reference CPU path's.  The
+  draws go straight from the generator into the step (pbh_legacy_run: one
+  fused kernel per launch; PBH_LEGACY_FUSED=0 runs stream generation + the
+  REPLAY kernel instead).  Timed like the headline (barrier + sync on both
+  sides, max over ranks): generation and the replay steps of exactly `steps`
+  steps, the full trace written.  Returns chain-steps/s of the whole job (not
+  `value`)."""
   from probayes_amd.dist import shard
   offset, n = shard(chains_per_gpu * world, rank, world)
   eng = make_engine()
@@ -301,12 +304,7 @@ def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup
   eng.reserve_replay(max(chunk, min(spl, warmup) if warmup else 1))
 
   def advance(k):
-    done = 0
-    while done < k:
-      m = min(chunk, k - done)
-      eng.legacy_replay(m)   # the next m rows of every chain's stream
-      eng.run(m, sync=False)
-      done += m
+    eng.legacy_run(k, steps_per_launch=chunk, sync=False)
 
   def barrier():
     eng.sync()
@@ -462,8 +460,9 @@ def main():
       line['replay_config'] = ('REPLAY: per-chain NumPy RandomState(global '
                                'chain id) streams generated on the device '
                                '(MT19937 + polar legacy gauss) and the '
-                               'reference arithmetic; stream generation '
-                               'inside the timed region')
+                               'reference arithmetic; generation inside the '
+                               'timed region, fused into the step '
+                               '(pbh_legacy_run)')
     if cpu is not None:
       line['cpu_baseline'] = cpu
     print(json.dumps(line), flush=True)

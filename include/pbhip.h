@@ -267,6 +267,15 @@ int pbh_legacy_replay(pbh_engine *eng, int64_t n_steps);
 int pbh_reserve_replay(pbh_engine *eng, int64_t n_steps);
 int pbh_get_replay(pbh_engine *eng, int64_t first, int64_t n_steps,
                    int32_t draw, double *out);
+/* pbh_legacy_replay(n) followed by pbh_run(n), in one kernel per launch:
+ * each step's draws are generated into the step's registers and never
+ * written to HBM.  The chains, trace, moments and legacy generator state are
+ * those of generation + run chunk by chunk (steps_per_launch as pbh_run);
+ * forms the fused kernel does not cover (Gibbs, per-variable deltas, a
+ * permuted draw order, a d without an instantiation) run that way.  REPLAY
+ * RNG, after pbh_legacy_seed.  No replay rows are held afterwards.  Replaces
+ * the reference's per-step np.random draws + SP.next (sp.py:221-258).      */
+int pbh_legacy_run(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
 
 /* ---- running (SP.walk / sample_generator: sp.py:281-295, sp_utils.py:8-16) */
 /* Device trace ring for the next runs: every thin-th step is recorded.

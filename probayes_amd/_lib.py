@@ -89,6 +89,7 @@ SIGNATURES = {
     'pbh_legacy_seed': (ctypes.c_int, [ctypes.c_void_p, _u32p]),
     'pbh_legacy_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     'pbh_reserve_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    'pbh_legacy_run': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),
     'pbh_get_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_int64, ctypes.c_int32, _dp]),
     'pbh_alloc_trace': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,

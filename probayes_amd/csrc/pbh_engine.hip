@@ -54,6 +54,7 @@ struct pbh_engine {
   bool legacy_db = true;       // PBH_LEGACY_DB=0: the in-place state
   bool legacy_k4 = true;       // PBH_LEGACY_K4=0: the round-3 double-buffered state
   bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
+  bool legacy_fused = true;    // PBH_LEGACY_FUSED=0: pbh_legacy_run as generation + run
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
   bool mt_stale = false;       // pbh_restore ran: the streams wait for
@@ -434,6 +435,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *ld = std::getenv("PBH_LEGACY_DB")) e->legacy_db = std::atoi(ld) != 0;
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   if (const char *lk = std::getenv("PBH_LEGACY_K4")) e->legacy_k4 = std::atoi(lk) != 0;
+  if (const char *lf = std::getenv("PBH_LEGACY_FUSED")) e->legacy_fused = std::atoi(lf) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
   // A/B switch for the markers' fences; default 0 = hipEventDefault)
   unsigned ev_flags = 0;
@@ -1155,38 +1157,14 @@ extern "C" int pbh_phase_dump(uint64_t *dst, int64_t words) {
 }
 #endif
 
-int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
-  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
-  // PBH_TRACE_ENQUEUE=1: the host time of each enqueue phase to stderr
-  // (diagnostic of short-launch latency)
-  static const bool trace_enq = [] {
-    const char *t = std::getenv("PBH_TRACE_ENQUEUE");
-    return t && t[0] == '1';
-  }();
-  using clk = std::chrono::steady_clock;
-  const auto tq0 = clk::now();
-  auto tq = [&](const char *what) {
-    if (trace_enq)
-      std::fprintf(stderr, "pbh_run %s %.2f us\n", what,
-                   std::chrono::duration<double, std::micro>(clk::now() - tq0).count());
-  };
+// pbh_run's (and pbh_legacy_run's) argument checks
+static int run_checks(pbh_engine *e, int64_t n_steps) {
   if (!e->has_model || (!e->has_prop && !e->has_gibbs))
     return fail(PBH_ERR_STATE, "model and proposal/gibbs tables must be set");
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (e->has_gibbs != (e->k.scores == PBH_SCORES_GIBBS))
     return fail(PBH_ERR_STATE, "gibbs scores need gibbs tables and vice versa");
   if (n_steps < 0) return fail(PBH_ERR_ARG, "n_steps < 0");
-  if (n_steps == 0) {
-    e->timed = false;
-    e->last_launches = 0;
-    return PBH_OK;
-  }
-  if (e->rng == PBH_RNG_REPLAY &&
-      (!e->rep || e->g < e->rep_g0 || e->g + n_steps > e->rep_g0 + e->rep_steps))
-    return fail(PBH_ERR_STATE,
-                "replay stream covers steps [%lld, %lld), run needs [%lld, %lld)",
-                (long long)e->rep_g0, (long long)(e->rep_g0 + e->rep_steps),
-                (long long)e->g, (long long)(e->g + n_steps));
   if (e->rng == PBH_RNG_PHILOX_FP32 && e->has_gibbs)
     return fail(PBH_ERR_UNSUPPORTED, "PHILOX_FP32 is a lane-pair MH comparison mode");
   if (e->cap > 0) {
@@ -1195,34 +1173,14 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
       return fail(PBH_ERR_STATE, "trace capacity %lld < %lld records",
                   (long long)e->cap, (long long)recs);
   }
-  // a running server and a run of its form: the command straight away (no
-  // kernel-argument block, no device call; the server's form was checked at
-  // its launch and every entry point that could change it stops it)
-  if (e->srv_active && (steps_per_launch <= 0 || steps_per_launch >= n_steps) &&
-      n_steps <= (1 << 30) && e->g + n_steps < (int64_t(1) << 47) &&
-      !(e->collect & PBH_COLLECT_MOMENTS) && e->has_pred && e->cap > 0 && e->thin == 1 &&
-      e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap) {
-    if (e->srv_pending) {
-      const int rc = srv_wait(e, e->srv_pending, false);
-      e->srv_pending = 0;
-      e->srv_last = srv_clk::now();
-      if (rc) return rc;
-    }
-    if (srv_clk::now() - e->srv_last <= std::chrono::milliseconds(e->srv_idle_ms / 2)) {
-      const bool short_run = n_steps <= 64;
-      srv_submit(e, n_steps, short_run ? e->fair_short : e->fair,
-                 short_run ? 1 : e->fair_rel);
-      tq("server command (fast path)");
-      return PBH_OK;
-    }
-  }
-  HIP_TRY(hipSetDevice(e->device));
-  if (e->rng == PBH_RNG_XOSHIRO && !e->xo_seeded) {
-    HIP_TRY(pbh::launch_xo_seed(e->xo, e->n, e->off, e->seed, e->stream));
-    e->xo_seeded = true;
-  }
-  const int64_t spl = steps_per_launch > 0 ? steps_per_launch : n_steps;
-  KArgs k = e->k;
+  return PBH_OK;
+}
+
+// a run's kernel arguments (the per-launch fields g0, n_steps, has_pred,
+// rep_row0, gq_init, lx, lx_init, fair, fair_rel are set per launch) and the
+// dynamic LDS of the NORM_IID observation stage
+static void run_args(pbh_engine *e, KArgs &k, size_t &lds) {
+  k = e->k;
   k.n = e->n;
   k.off = e->off;
   k.x = e->x;
@@ -1269,13 +1227,72 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   k.fair = e->fair;
   k.pair_wg = e->pair_wg;
   k.gq = e->gq;
-  const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   k.moments = (e->collect & PBH_COLLECT_MOMENTS) ? 1 : 0;
   k.msum = e->msum; k.msq = e->msq; k.nacc = e->nacc;
   k.bm64 = e->bm64;
-  const size_t lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
+  lds = (k.target == PBH_TARGET_NORM_IID && k.tn <= 16384 &&
                       k.rng != PBH_RNG_PHILOX)   // production: O(1) statistics
                          ? (size_t)k.tn * sizeof(double) : 0;
+}
+
+int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  // PBH_TRACE_ENQUEUE=1: the host time of each enqueue phase to stderr
+  // (diagnostic of short-launch latency)
+  static const bool trace_enq = [] {
+    const char *t = std::getenv("PBH_TRACE_ENQUEUE");
+    return t && t[0] == '1';
+  }();
+  using clk = std::chrono::steady_clock;
+  const auto tq0 = clk::now();
+  auto tq = [&](const char *what) {
+    if (trace_enq)
+      std::fprintf(stderr, "pbh_run %s %.2f us\n", what,
+                   std::chrono::duration<double, std::micro>(clk::now() - tq0).count());
+  };
+  if (const int rc = run_checks(e, n_steps)) return rc;
+  if (n_steps == 0) {
+    e->timed = false;
+    e->last_launches = 0;
+    return PBH_OK;
+  }
+  if (e->rng == PBH_RNG_REPLAY &&
+      (!e->rep || e->g < e->rep_g0 || e->g + n_steps > e->rep_g0 + e->rep_steps))
+    return fail(PBH_ERR_STATE,
+                "replay stream covers steps [%lld, %lld), run needs [%lld, %lld)",
+                (long long)e->rep_g0, (long long)(e->rep_g0 + e->rep_steps),
+                (long long)e->g, (long long)(e->g + n_steps));
+  // a running server and a run of its form: the command straight away (no
+  // kernel-argument block, no device call; the server's form was checked at
+  // its launch and every entry point that could change it stops it)
+  if (e->srv_active && (steps_per_launch <= 0 || steps_per_launch >= n_steps) &&
+      n_steps <= (1 << 30) && e->g + n_steps < (int64_t(1) << 47) &&
+      !(e->collect & PBH_COLLECT_MOMENTS) && e->has_pred && e->cap > 0 && e->thin == 1 &&
+      e->g - e->rec_base >= 0 && e->g + n_steps - e->rec_base <= e->cap) {
+    if (e->srv_pending) {
+      const int rc = srv_wait(e, e->srv_pending, false);
+      e->srv_pending = 0;
+      e->srv_last = srv_clk::now();
+      if (rc) return rc;
+    }
+    if (srv_clk::now() - e->srv_last <= std::chrono::milliseconds(e->srv_idle_ms / 2)) {
+      const bool short_run = n_steps <= 64;
+      srv_submit(e, n_steps, short_run ? e->fair_short : e->fair,
+                 short_run ? 1 : e->fair_rel);
+      tq("server command (fast path)");
+      return PBH_OK;
+    }
+  }
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->rng == PBH_RNG_XOSHIRO && !e->xo_seeded) {
+    HIP_TRY(pbh::launch_xo_seed(e->xo, e->n, e->off, e->seed, e->stream));
+    e->xo_seeded = true;
+  }
+  const int64_t spl = steps_per_launch > 0 ? steps_per_launch : n_steps;
+  KArgs k;
+  size_t lds = 0;
+  run_args(e, k, lds);
+  const bool gfast = e->has_gibbs && pbh::gibbs_fast_form(k);
   // the resident server: one command for the whole run when the run is one
   // steady-state lane-pair launch (launch_mh_server's check); anything else
   // stops a running server and launches normally
@@ -1373,6 +1390,111 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   tq("launches");
   if (e->event_markers) HIP_TRY(hipEventRecord(e->ev1, e->stream));
   tq("event1");
+  e->mom_steps += n_steps;
+  e->timed = true;
+  e->last_launches = launches;
+  return PBH_OK;
+}
+
+// Generation and the REPLAY chain-step in one kernel per launch (pbh_legacy.hip
+// legacy_mh_kernel): the draws never pass through HBM.  Same chains, trace
+// and legacy state as pbh_legacy_replay + pbh_run chunk by chunk, which is
+// what runs for the forms the fused kernel does not cover (Gibbs, per-
+// variable deltas, a permuted draw order, the pre-Mt4 state layouts, a d
+// without an instantiation) and with PBH_LEGACY_FUSED=0.  The stream buffer
+// is not written: afterwards no replay rows are held (pbh_get_replay).
+int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  if (e->rng != PBH_RNG_REPLAY)
+    return fail(PBH_ERR_STATE, "pbh_legacy_run runs the REPLAY RNG (pbh_set_rng)");
+  if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first");
+  if (e->mt_stale)
+    return fail(PBH_ERR_STATE, "pbh_restore ran after pbh_legacy_seed: set the "
+                "checkpoint's legacy state (pbh_set_legacy_state) first");
+  if (const int rc = run_checks(e, n_steps)) return rc;
+  if (n_steps == 0) {
+    e->timed = false;
+    e->last_launches = 0;
+    return PBH_OK;
+  }
+  const int64_t spl = steps_per_launch > 0 ? steps_per_launch : n_steps;
+  int32_t R = 0;
+  if (const int rc = pbh_stream_width(e, &R)) return rc;
+  HIP_TRY(hipSetDevice(e->device));
+  KArgs k;
+  size_t lds = 0;
+  run_args(e, k, lds);
+  if (!e->lgtab) {
+    std::vector<double> lt(pbh::kLegLogDoubles);
+    pbh::legacy_log_table(lt.data());
+    if (const int rc = dalloc(e->lgtab, lt.size())) return rc;
+    HIP_TRY(hipMemcpy(e->lgtab, lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  pbh::LegacyArgs la{};
+  la.key = e->mt_key; la.pos = e->mt_pos; la.gauss = e->mt_gauss;
+  la.has_gauss = e->mt_has; la.order = nullptr; la.out = nullptr;
+  la.n = e->n; la.d = e->d; la.R = R; la.gibbs = e->has_gibbs ? 1 : 0;
+  la.normal = (!e->has_gibbs && e->k.prop == PBH_PROP_GAUSS) ? 1 : 0;
+  la.vardelta = (!e->has_gibbs && e->k.prop == PBH_PROP_VARDELTA) ? 1 : 0;
+  la.db = e->mt_mode;
+  la.win = e->legacy_win ? 1 : 0;
+  la.lgtab = e->lgtab;
+  bool ident = true;
+  for (int j = 0; j < (int)e->draw_order.size(); ++j) ident = ident && e->draw_order[j] == j;
+  const bool fused = e->legacy_fused && ident &&
+                     pbh::launch_legacy_mh(la, k, e->stream, true) == hipSuccess;
+  if (!fused) {
+    for (int64_t done = 0; done < n_steps;) {
+      const int64_t m = std::min(spl, n_steps - done);
+      int rc = pbh_legacy_replay(e, m);
+      if (!rc) rc = pbh_run(e, m, 0);
+      if (rc) return rc;
+      done += m;
+    }
+    return PBH_OK;
+  }
+  e->srv_timed = false;
+  pbh::LaunchEvents &lev = pbh::launch_events();
+  if (e->event_markers) {
+    HIP_TRY(hipEventRecord(e->ev0, e->stream));
+    lev = {};
+  } else {
+    lev.start = e->ev0;
+    lev.stop = nullptr;
+  }
+  // launches of at most 2^20 steps, as pbh_legacy_replay (Mt4's 32-bit head)
+  constexpr int64_t kLegacyLaunchSteps = int64_t(1) << 20;
+  int64_t launches = 0;
+  for (int64_t done = 0; done < n_steps;) {
+    const int64_t m = std::min(std::min(spl, kLegacyLaunchSteps), n_steps - done);
+    if (!e->event_markers && done + m >= n_steps) lev.stop = e->ev1;
+    k.n_steps = (int32_t)m;
+    k.g0 = e->g;
+    k.has_pred = e->has_pred ? 1 : 0;
+    k.rep_row0 = 0;
+    k.lx = e->lx;
+    k.lx_init = 1;
+    la.n_steps = m;
+    la.step0 = e->g;
+    const hipError_t err = pbh::launch_legacy_mh(la, k, e->stream, false);
+    if (err != hipSuccess) {
+      lev = {};
+      return fail(PBH_ERR_HIP, "pbh_legacy_run: %s", hipGetErrorString(err));
+    }
+    e->g += m;
+    e->has_pred = true;
+    done += m;
+    ++launches;
+  }
+  lev = {};
+  if (e->event_markers) HIP_TRY(hipEventRecord(e->ev1, e->stream));
+  e->gq_valid = false;
+  e->lx_valid = false;
+  // the stream rows are not written: none are held from here on
+  e->k.R = R;
+  e->rep_steps = 0;
+  e->rep_g0 = e->g;
   e->mom_steps += n_steps;
   e->timed = true;
   e->last_launches = launches;

@@ -240,6 +240,11 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
                               int64_t n, int32_t db, hipStream_t s);
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s);
+// The fused REPLAY kernel: generation and the REPLAY chain-step in one
+// launch (la: the generator's state, a: the run's kernel arguments, a.n_steps
+// = la.n_steps).  hipErrorNotSupported: the form is not covered (the caller
+// runs launch_legacy_gen + launch_mh); check: report only.
+hipError_t launch_legacy_mh(const LegacyArgs &la, const KArgs &a, hipStream_t s, bool check);
 
 // bool_perm_freq histogram (pbh_likelihoods.hip); counts must be zeroed,
 // scratch holds bool_perm_scratch_words(n_cu) u64 partials.

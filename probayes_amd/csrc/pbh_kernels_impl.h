@@ -434,8 +434,27 @@ __device__ __forceinline__ double randint_u(double u, double d0) {
 // ---------------------------------------------------------------------------
 // MH kernel: n_steps fused chain-steps, one chain per lane
 // ---------------------------------------------------------------------------
-template <int D, int RNG, int TGT, int PROP>
-__global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
+// REPLAY's draws of step s: row rep_row0 + s of the [T][R][N] stream (d
+// draws in dim order, then the threshold).  The fused legacy kernel
+// (pbh_legacy.hip legacy_mh_kernel) supplies another source that generates
+// the same values in registers.
+struct RowDraws {
+  __device__ __forceinline__ void begin() {}
+  template <int D>
+  __device__ __forceinline__ void draws(const KArgs &a, int s, int64_t cc, double (&r)[D],
+                                        double &thr) {
+    const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
+#pragma unroll
+    for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
+    thr = row[(int64_t)D * a.n];
+  }
+};
+
+// The kernel body; SRC supplies REPLAY's draws, s_obs is the workgroup's
+// LDS for NORM_IID observations (lds_ok: the caller reserved a.tn doubles)
+template <int D, int RNG, int TGT, int PROP, class SRC>
+__device__ __forceinline__ void mh_body(const KArgs &a, SRC &src, double *s_obs,
+                                        bool lds_ok) {
   // TGT / PROP != 0 compile the kernel for one target / proposal form;
   // 0 keeps the wave-uniform runtime switch (any model, one binary).
   // FAST = production Philox path (fp32 normals, FMA-corrected divisions);
@@ -449,7 +468,6 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   const bool mom = a.moments != 0;
   // production modes with the symmetric ratio form: the acceptance filter
   const bool simple = FAST && a.simple_acc && !a.debug;
-  extern __shared__ double s_obs[];
   __shared__ double s_bmt[TAB ? kBm64Doubles : 2];
   if constexpr (TAB) bm64_load(s_bmt, a.bm64);
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -458,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   const int lane = threadIdx.x & 63;
 
   bool use_lds = false;
-  if (!FAST && (TGT == 0 || TGT == PBH_TARGET_NORM_IID) &&
+  if (!FAST && (TGT == 0 || TGT == PBH_TARGET_NORM_IID) && lds_ok &&
       a.target == PBH_TARGET_NORM_IID && a.tn <= 16384) {
     for (int64_t j = threadIdx.x; j < a.tn; j += kBlock) s_obs[j] = cld(a.ta, j);
     __syncthreads();
@@ -493,6 +511,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
   // record (g + 1) / thin - 1 - rec_base.
   int ph = (int)((a.g0 + 1) % a.thin);
   int64_t ri = (a.g0 + 1) / a.thin - 1 - a.rec_base;
+  if (RNG == PBH_RNG_REPLAY) src.begin();
   for (int s = 0; s < a.n_steps; ++s) {
     const int64_t g = a.g0 + s;
     // ---- draws ----
@@ -504,10 +523,7 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     uint32_t lead = 0, lead_ctr = 0;
     int lead_bits = 0;
     if (RNG == PBH_RNG_REPLAY) {
-      const double *row = a.rep + (a.rep_row0 + s) * a.R * a.n + cc;
-#pragma unroll
-      for (int k = 0; k < D; ++k) r[k] = row[k * a.n];
-      thr = row[(int64_t)D * a.n];
+      src.template draws<D>(a, s, cc, r, thr);
     } else if (RNG == PBH_RNG_XOSHIRO) {
       // three words per normal pair, two per 53-bit uniform, in draw order
       if (prop == PBH_PROP_GAUSS) {
@@ -763,6 +779,13 @@ __global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
     }
     if (RNG == PBH_RNG_XOSHIRO) xo_store(a, 0, c, xs);
   }
+}
+
+template <int D, int RNG, int TGT, int PROP>
+__global__ __launch_bounds__(kBlock) void mh_kernel(KArgs a) {
+  extern __shared__ double s_obs[];
+  RowDraws src;
+  mh_body<D, RNG, TGT, PROP>(a, src, s_obs, true);
 }
 
 // ---------------------------------------------------------------------------

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "pbh_kernels.h"
+#include "pbh_kernels_impl.h"   // mh_body: the fused REPLAY kernel
 #include "pbhip.h"
 
 namespace pbh {
@@ -1087,6 +1088,91 @@ __device__ __forceinline__ double log_leg(double x, const double *tab) {
   return shi + (r + p);
 }
 
+// The polar method's attempts of one step (legacy_gauss's draws): lanes run
+// the ATTEMPTS in lockstep (one per iteration until each holds its `need`
+// pairs: a wave loops ~max over lanes of the step's attempts, about 9.5 for 5
+// pairs, not the sum over pairs of per-pair maxima, about 18), keeping only
+// the accepted (x1, x2) in LDS, [pair][thread].
+template <class M>
+__device__ __forceinline__ void polar_attempts(M &m, int need, double2 *stage) {
+  int np = 0;
+  if constexpr (M::kPeek && M::kPeek4) {
+    // four attempts per lockstep iteration from the staged doubles
+    // (~3 iterations for 5 pairs), consumed only as far as they are used
+    while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+      if (np < need) {
+        double x1[4], x2[4];
+        m.attempts4(x1, x2);
+        int used = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double r2 = x1[i] * x1[i] + x2[i] * x2[i];
+          if (np < need) {
+            used += 4;
+            if (r2 < 1.0 && r2 != 0.0) {
+              stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1[i], x2[i]);
+              ++np;
+            }
+          }
+        }
+        m.advance(used);
+      }
+    }
+  } else if constexpr (M::kPeek) {
+    // two attempts per lockstep iteration (read ahead from the window,
+    // consumed only as far as they are used): ~5.5 iterations for 5
+    // pairs instead of ~9.5, and two independent chains of arithmetic
+    while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+      if (np < need) {
+        double x1a, x2a, x1b, x2b;
+        m.attempts2(x1a, x2a, x1b, x2b);
+        const double r2a = x1a * x1a + x2a * x2a;
+        const double r2b = x1b * x1b + x2b * x2b;
+        if (r2a < 1.0 && r2a != 0.0) {
+          stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1a, x2a);
+          ++np;
+        }
+        int used = 4;
+        if (np < need) {
+          used = 8;
+          if (r2b < 1.0 && r2b != 0.0) {
+            stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1b, x2b);
+            ++np;
+          }
+        }
+        m.advance(used);
+      }
+    }
+  } else {
+    while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
+      if (np < need) {
+        const double x1 = 2.0 * m.next_double() - 1.0;
+        const double x2 = 2.0 * m.next_double() - 1.0;
+        const double r2 = x1 * x1 + x2 * x2;
+        if (r2 < 1.0 && r2 != 0.0) {
+          stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1, x2);
+          ++np;
+        }
+      }
+    }
+  }
+}
+
+// The transcendental part of accepted pair k: f = sqrt(-2 ln r2 / r2), the
+// deviates (f x2, f x1) in legacy_gauss's order.
+template <class M>
+__device__ __forceinline__ void polar_pair(const double2 *stage, int k, const double *s_lg,
+                                           double &g0, double &g1) {
+  const double2 p = stage[k * kBlockLegacy + threadIdx.x];
+  const double r2 = p.x * p.x + p.y * p.y;
+  double lr;
+  if constexpr (M::kLogTab) lr = log_leg(r2, s_lg);   // Mt4: the table log
+  else lr = log(r2);
+  const double f = sqrt(-2.0 * lr / r2);
+  g0 = f * p.y;
+  g1 = f * p.x;
+}
+
 // s_ord (the windowed kernels): order[j] n per draw j, staged in LDS at the
 // kernel's start.  Read from a.order, every row index was a vector load
 // whose s_waitcnt vmcnt(0) also waited for the step's earlier trace stores
@@ -1159,67 +1245,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
         j0 = 1;
       }
       const int need = (a.d - j0 + 1) / 2;   // pairs this lane draws
-      int np = 0;
-      if constexpr (M::kPeek && M::kPeek4) {
-        // four attempts per lockstep iteration from the staged doubles
-        // (~3 iterations for 5 pairs), consumed only as far as they are used
-        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
-          if (np < need) {
-            double x1[4], x2[4];
-            m.attempts4(x1, x2);
-            int used = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const double r2 = x1[i] * x1[i] + x2[i] * x2[i];
-              if (np < need) {
-                used += 4;
-                if (r2 < 1.0 && r2 != 0.0) {
-                  stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1[i], x2[i]);
-                  ++np;
-                }
-              }
-            }
-            m.advance(used);
-          }
-        }
-      } else if constexpr (M::kPeek) {
-        // two attempts per lockstep iteration (read ahead from the window,
-        // consumed only as far as they are used): ~5.5 iterations for 5
-        // pairs instead of ~9.5, and two independent chains of arithmetic
-        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
-          if (np < need) {
-            double x1a, x2a, x1b, x2b;
-            m.attempts2(x1a, x2a, x1b, x2b);
-            const double r2a = x1a * x1a + x2a * x2a;
-            const double r2b = x1b * x1b + x2b * x2b;
-            if (r2a < 1.0 && r2a != 0.0) {
-              stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1a, x2a);
-              ++np;
-            }
-            int used = 4;
-            if (np < need) {
-              used = 8;
-              if (r2b < 1.0 && r2b != 0.0) {
-                stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1b, x2b);
-                ++np;
-              }
-            }
-            m.advance(used);
-          }
-        }
-      } else {
-        while (__builtin_amdgcn_ballot_w64(np < need)) {   // wave-uniform
-          if (np < need) {
-            const double x1 = 2.0 * m.next_double() - 1.0;
-            const double x2 = 2.0 * m.next_double() - 1.0;
-            const double r2 = x1 * x1 + x2 * x2;
-            if (r2 < 1.0 && r2 != 0.0) {
-              stage[np * kBlockLegacy + threadIdx.x] = make_double2(x1, x2);
-              ++np;
-            }
-          }
-        }
-      }
+      polar_attempts(m, need, stage);
       // Wait here for this step's window prefetch (issued at the step top,
       // complete by now) and the previous step's trace stores (issued ~a step
       // ago): vmcnt(0) only, once per step, before this step's stores.  The
@@ -1233,16 +1259,7 @@ __device__ __forceinline__ void legacy_gen_body(const LegacyArgs &a, int64_t c, 
       // cached (odd d - j0) after them
       const int half = (a.d - j0) & 1;
       const int nfull = need - half;
-      auto polar = [&](int k, double &g0, double &g1) {
-        const double2 p = stage[k * kBlockLegacy + threadIdx.x];
-        const double r2 = p.x * p.x + p.y * p.y;
-        double lr;
-        if constexpr (M::kLogTab) lr = log_leg(r2, s_lg);   // Mt4: the table log
-        else lr = log(r2);
-        const double f = sqrt(-2.0 * lr / r2);
-        g0 = f * p.y;
-        g1 = f * p.x;
-      };
+      auto polar = [&](int k, double &g0, double &g1) { polar_pair<M>(stage, k, s_lg, g0, g1); };
       int k = 0;
       for (; k + 2 <= nfull; k += 2) {
         double a0, a1, b0, b1;
@@ -1389,6 +1406,133 @@ hipError_t launch_win(const LegacyArgs &a, hipStream_t s) {
   return launch_win_mode<H, kModeRaw>(a, s);
 }
 
+// ---------------------------------------------------------------------------
+// Fused REPLAY (legacy_mh_kernel): the generator and the REPLAY chain-step in
+// one kernel.  The two-kernel form writes the [T][R][N] stream (1.44 GB per
+// 250 cfg2-width steps) and the REPLAY kernel reads it back; here each
+// step's draws go from the Mt4 window straight into the step's registers.
+// mh_body (pbh_kernels_impl.h) is the REPLAY kernel's own body -- the same
+// proposal, density, score and trace code -- with LegacyDraws as its draw
+// source, which runs legacy_gen_body's per-step generation for the normal
+// (callable Gaussian Delta) and raw (tuple / list delta) modes with the
+// identity draw order (draw j feeds dim j): the values, their order and the
+// cached deviate are the stream kernel's, so chains, traces and the legacy
+// state equal legacy_replay + run.  Lanes past the last chain leave at once
+// (the generator's ballots count active lanes only), so mh_body sees active
+// lanes only and runs without the LDS observation stage (its
+// __syncthreads); one chain per lane at one wavefront per SIMD (the window
+// and the polar stage take ~155 KB of LDS per 256 lanes).
+// ---------------------------------------------------------------------------
+template <class M, bool NORMAL>
+struct LegacyDraws {
+  M &m;
+  double2 *stage;
+  const double *s_lg;
+  double gauss;
+  int has;
+
+  // every load before the step loop completes here, once (see legacy_gen_body)
+  __device__ __forceinline__ void begin() { __builtin_amdgcn_s_waitcnt(0); }
+
+  // the step's D normals with J0 = 1 when the cached deviate leads
+  template <int D, int J0>
+  __device__ __forceinline__ void normals(double (&r)[D]) {
+    constexpr int need = (D - J0 + 1) / 2, half = (D - J0) & 1, nfull = need - half;
+    if constexpr (J0 == 1) {
+      r[0] = gauss;
+      has = 0;
+      gauss = 0.0;
+    }
+    polar_attempts(m, need, stage);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): as legacy_gen_body
+#pragma unroll
+    for (int k = 0; k < nfull; ++k) {
+      double g0, g1;
+      polar_pair<M>(stage, k, s_lg, g0, g1);
+      r[J0 + 2 * k] = g0;
+      r[J0 + 2 * k + 1] = g1;
+    }
+    if constexpr (half != 0) {
+      double g0, g1;
+      polar_pair<M>(stage, nfull, s_lg, g0, g1);
+      r[J0 + 2 * nfull] = g0;
+      gauss = g1;   // cached for the next draw (odd d)
+      has = 1;
+    }
+  }
+
+  template <int D>
+  __device__ __forceinline__ void draws(const KArgs &, int, int64_t, double (&r)[D],
+                                        double &thr) {
+    m.maintain();   // wave-uniform: every active lane is here
+    if constexpr (NORMAL) {
+      // the same flag in every lane (each chain draws D per step from the
+      // same start): wave-uniform
+      has = __builtin_amdgcn_readfirstlane(has);
+      if (has) normals<D, 1>(r);
+      else normals<D, 0>(r);
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) r[k] = m.next_double();
+    }
+    thr = m.next_double();   // the MH threshold
+  }
+};
+
+template <int D, int H, bool NORMAL, int TGT, int PROP>
+__global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void legacy_mh_kernel(LegacyArgs la, KArgs a) {
+  static_assert(kBlockLegacy == kBlock, "mh_body's chain index");
+  extern __shared__ w4 s_lw[];
+  __shared__ double s_lg[kLegLogDoubles];
+  for (int i = threadIdx.x; i < kLegLogDoubles; i += kBlockLegacy) s_lg[i] = la.lgtab[i];
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
+  if (c >= la.n) return;
+  using M = Mt4<H, true>;
+  M m;
+  m.key = reinterpret_cast<w4 *>(la.key);
+  m.n = la.n;
+  m.c = c;
+  m.init(la.pos[c], s_lw + threadIdx.x);
+  LegacyDraws<M, NORMAL> src{m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_lg,
+                             la.gauss[c], la.has_gauss[c]};
+  mh_body<D, PBH_RNG_REPLAY, TGT, PROP>(a, src, nullptr, false);
+  la.pos[c] = m.packed();
+  la.gauss[c] = src.gauss;
+  la.has_gauss[c] = src.has;
+}
+
+template <int D, int H, bool NORMAL, int TGT, int PROP>
+hipError_t launch_legacy_mh_t(const LegacyArgs &la, const KArgs &a, hipStream_t s) {
+  const void *fn = reinterpret_cast<const void *>(&legacy_mh_kernel<D, H, NORMAL, TGT, PROP>);
+  const size_t lds = (size_t)(2 * H + (NORMAL ? (D + 1) / 2 : 0)) * kBlockLegacy * sizeof(uint4);
+  static const hipError_t attr =
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  const dim3 grid((unsigned)((la.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+  // the timed region's events on the dispatch packet, as pbh_launch
+  LaunchEvents &ev = launch_events();
+  if (ev.start || ev.stop)
+    (void)hipExtLaunchKernelGGL((legacy_mh_kernel<D, H, NORMAL, TGT, PROP>), grid, block,
+                                (uint32_t)lds, s, ev.start, ev.stop, 0u, la, a);
+  else
+    hipLaunchKernelGGL((legacy_mh_kernel<D, H, NORMAL, TGT, PROP>), grid, block, lds, s, la, a);
+  ev.start = nullptr;
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_legacy_mh_d(const LegacyArgs &la, const KArgs &a, hipStream_t s) {
+  constexpr int H = D <= 12 ? 16 : 8;   // the window while the stage leaves room
+  if (la.normal) {
+    if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS)   // cfg2's form
+      return launch_legacy_mh_t<D, H, true, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>(la, a, s);
+    return launch_legacy_mh_t<D, H, true, 0, 0>(la, a, s);
+  }
+  return launch_legacy_mh_t<D, 16, false, 0, 0>(la, a, s);
+}
+
 }  // namespace
 
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
@@ -1423,6 +1567,34 @@ hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
   else
     hipLaunchKernelGGL(legacy_gen_kernel, grid, block, 0, s, a);
   return hipGetLastError();
+}
+
+// The fused REPLAY kernel for the forms it covers (see legacy_mh_kernel):
+// Mt4 state, MH with normal or raw draws, identity draw order, d of an
+// instantiated kernel.  check: only report whether it applies.
+bool legacy_mh_dim(int d) {
+  switch (d) {
+    case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 10: return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_legacy_mh(const LegacyArgs &la, const KArgs &a, hipStream_t s, bool check) {
+  if (la.db != 2 || la.gibbs || la.vardelta || la.d != a.d || !legacy_mh_dim(la.d) ||
+      !(la.normal ? a.prop == PBH_PROP_GAUSS
+                  : (a.prop == PBH_PROP_UNIFORM || a.prop == PBH_PROP_SPHERE)))
+    return hipErrorNotSupported;
+  if (check) return hipSuccess;
+  switch (la.d) {
+    case 1: return launch_legacy_mh_d<1>(la, a, s);
+    case 2: return launch_legacy_mh_d<2>(la, a, s);
+    case 3: return launch_legacy_mh_d<3>(la, a, s);
+    case 4: return launch_legacy_mh_d<4>(la, a, s);
+    case 5: return launch_legacy_mh_d<5>(la, a, s);
+    case 6: return launch_legacy_mh_d<6>(la, a, s);
+    case 8: return launch_legacy_mh_d<8>(la, a, s);
+    default: return launch_legacy_mh_d<10>(la, a, s);
+  }
 }
 
 }  // namespace pbh

@@ -289,6 +289,15 @@ class Engine:
     if sync:
       self.sync()
 
+  def legacy_run(self, n_steps, steps_per_launch=0, sync=True):
+    """legacy_replay(n) + run(n) in one kernel per launch (the draws go
+    from each chain's device RandomState straight into the step): the same
+    chains, trace and generator state; no replay rows are held afterwards."""
+    _lib.call('pbh_legacy_run', self._h, _c.c_int64(int(n_steps)),
+              int(steps_per_launch))
+    if sync:
+      self.sync()
+
   def sync(self):
     _lib.call('pbh_sync', self._h)
 

@@ -313,6 +313,9 @@ class MainEngine(OracleEngine):
     assert k >= 1
   def reserve_replay(self, k):
     assert k >= 1
+  def legacy_run(self, k, steps_per_launch=0, sync=True):
+    assert k >= 1 and steps_per_launch >= 1
+    self.run(k, steps_per_launch, sync)
   def close(self):
     if getattr(self, 'col', None) is not None:
       self.col.close()
