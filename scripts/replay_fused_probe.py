@@ -18,7 +18,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 spl = int(sys.argv[3]) if len(sys.argv) > 3 else 250
 
-for form in ('fused', 'two_kernel'):
+forms = sys.argv[4].split(',') if len(sys.argv) > 4 else ['fused', 'two_kernel']
+for form in forms:
   eng = Engine(bench.cfg2_spec())
   eng.init_chains(np.zeros((n, bench.D)))
   eng.set_rng('replay')
@@ -41,6 +42,6 @@ for form in ('fused', 'two_kernel'):
   eng.sync()
   el = time.perf_counter() - t0
   eng.close()
-  print(json.dumps({'form': form, 'n': n, 'steps': steps, 'spl': spl,
+  print(json.dumps({'form': form, 'pair': os.environ.get('PBH_LEGACY_PAIR', '1'), 'n': n, 'steps': steps, 'spl': spl,
                     'ms_per_launch': el * 1e3 / (steps / spl),
                     'chain_steps_per_s': n * steps / el}), flush=True)
