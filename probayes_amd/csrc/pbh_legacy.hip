@@ -715,12 +715,14 @@ __device__ __forceinline__ int mt4_stage(w4 *key, int64_t n, int64_t c, w4 *win,
 // line; the head's block is twisted first if nothing has (values in and out:
 // returns (ready << 32) | hq, each a full 32-bit field: hq counts the launch's
 // quads per chain and grows past 2^24 in a launch of a few million steps)
-template <int H, bool DBL>
+// (NC chunks: H / 8 when the window is nearly empty, the regular refill's
+// kRC at a step top)
+template <int H, bool DBL, int NC = H / 8>
 __device__ __attribute__((noinline)) uint64_t mt4_refill_cold(w4 *key, int64_t n, int64_t c,
                                                          w4 *win, int hq, int blk, int cb,
                                                          int ready) {
 #pragma unroll 1
-  for (int k = 0; k < H / 8; ++k) {
+  for (int k = 0; k < NC; ++k) {
     const int hb = hq / kQ, hc = (hq - hb * kQ) >> 3;
     if (hb - blk > ready) {   // the head's block is not twisted yet
       mt4_twist_cold(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
@@ -731,6 +733,16 @@ __device__ __attribute__((noinline)) uint64_t mt4_refill_cold(w4 *key, int64_t n
   return ((uint64_t)(uint32_t)ready << 32) | (uint32_t)hq;
 }
 
+// Window refills of kRC chunks (PBH_LEGACY_RC, default 1): a lane stages
+// its next chunk whenever the ring has room for it.  The lanes of a wave
+// reach their refills at different steps (they drift apart in the stream),
+// so a refill's code runs for the wave at nearly every step whoever needs it:
+// with two-chunk refills (16 quads, the round-4 form, PBH_LEGACY_RC=2) the
+// wave converted 16 quads' worth of doubles per step for ~7 quads consumed
+// per lane-step; with one-chunk refills it converts 8.
+#ifndef PBH_LEGACY_RC
+#define PBH_LEGACY_RC 1
+#endif
 template <int H, bool DBL = false>
 struct Mt4 {
   static constexpr bool kLockstep = true;
@@ -740,6 +752,10 @@ struct Mt4 {
   static constexpr int kRefill = 312;
   static constexpr int kW = 2 * H;      // window quads per lane (a power of two)
   static_assert(H % 8 == 0, "whole chunks per refill");
+  // chunks per regular refill (the cold path stages H / 8); a refill when
+  // the ring has room for them
+  static constexpr int kRC = PBH_LEGACY_RC < H / 8 ? PBH_LEGACY_RC : H / 8;
+  static constexpr int kRoom = kW - 8 * kRC;
   w4 *key;
   int64_t n, c;
   int pos, cb, ready;
@@ -750,7 +766,7 @@ struct Mt4 {
   w4 *win;      // this lane's slot 0 (slot stride blockDim.x)
   // the next refill's chunks, loaded one refill ahead (pf): their loads
   // complete during the steps in between instead of stalling the step top
-  w4 pfv[H / 8][8];
+  w4 pfv[kRC][8];
   bool pf;
 
   __device__ __forceinline__ w4 &slot(int k) {
@@ -758,8 +774,9 @@ struct Mt4 {
   }
   __device__ __forceinline__ int aq() const { return blk * kQ + (pos >> 2); }
 
+  template <int NC = H / 8>
   __device__ __forceinline__ void refill_cold() {
-    const uint64_t r = mt4_refill_cold<H, DBL>(key, n, c, win, hq, blk, cb, ready);
+    const uint64_t r = mt4_refill_cold<H, DBL, NC>(key, n, c, win, hq, blk, cb, ready);
     hq = (int)(uint32_t)r;
     ready = (int)(uint32_t)(r >> 32);
     hb = hq / kQ;
@@ -769,12 +786,12 @@ struct Mt4 {
 
   // the next refill's blocks are twisted
   __device__ __forceinline__ bool ahead_ok() const {
-    return (hb - blk) + (hc + H / 8 > kCh ? 1 : 0) <= ready;
+    return (hb - blk) + (hc + kRC > kCh ? 1 : 0) <= ready;
   }
   __device__ __forceinline__ void prefetch() {
     int b = hb, ch = hc;
 #pragma unroll
-    for (int k = 0; k < H / 8; ++k) {
+    for (int k = 0; k < kRC; ++k) {
       mt4_load(key, n, c, (cb + b - blk) & 3, ch, pfv[k]);
       if (++ch == kCh) {
         ch = 0;
@@ -785,7 +802,7 @@ struct Mt4 {
   }
   __device__ __forceinline__ void commit() {
 #pragma unroll
-    for (int k = 0; k < H / 8; ++k) {
+    for (int k = 0; k < kRC; ++k) {
       hq += mt4_put<DBL>(win, kW, hc, hq, pfv[k]);
       if (++hc == kCh) {
         hc = 0;
@@ -812,22 +829,22 @@ struct Mt4 {
 
   // wave-uniform point (top of a step): a twist round, then the window
   __device__ __forceinline__ void maintain() {
-    const bool due = ready == 0 && (pos >= kRefill || hb > blk || hc + H / 8 > kCh);
+    const bool due = ready == 0 && (pos >= kRefill || hb > blk || hc + kRC > kCh);
     if (__builtin_amdgcn_ballot_w64(due)) {
       if (ready < kK4 - 1) {   // every lane with a free buffer: one block further
         mt4_twist(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
         ++ready;
       }
     }
-    if (__builtin_amdgcn_ballot_w64(hq - aq() <= H)) {
-      if (hq - aq() <= H) {
+    if (__builtin_amdgcn_ballot_w64(hq - aq() <= kRoom)) {
+      if (hq - aq() <= kRoom) {
         // loaded ahead (complete since the last step's mid-step wait), or not
         // (its block was not twisted then): the same chunks staged out of
         // line, so that the common path's code carries no wait for loads
         // just issued (one shared commit waited vmcnt down to 0 -- i.e. for
         // the last step's trace stores -- on both paths)
         if (pf) commit();
-        else refill_cold();
+        else refill_cold<kRC>();   // (the ring has room for kRC chunks only)
       }
     }
     // the next refill, ahead (whenever its blocks are twisted)
