@@ -504,7 +504,13 @@ __device__ __forceinline__ double ln_tab(double S, const double *tab) {
 // exp(y) for y <= 0 (log-sum-exp terms): y = (n + i/64) ln 2 + r, |r| <=
 // ln2 / 128, exp(y) = 2^n 2^(i/64) poly5(r) from the 64-entry LDS table.
 // About 16 VALU, within 2 ulp; y < -745 gives 0.
-__device__ __forceinline__ double exp_tab(double y, const double *tab) {
+// (in two halves, exp_tab_pre / exp_tab_fin, so that a caller with several
+// independent terms can issue every table read before the first is used)
+struct ExpPre {
+  double p, t;
+  int ki;
+};
+__device__ __forceinline__ ExpPre exp_tab_pre(double y, const double *tab) {
   y = __builtin_fmax(y, -746.0);                             // -inf -> 0
   const double k = __builtin_rint(y * 92.332482616893656);   // 64 / ln 2
   // ln2/64 = hi + lo, hi with 36 significant bits: k hi exact for |k| < 2^17
@@ -516,8 +522,13 @@ __device__ __forceinline__ double exp_tab(double y, const double *tab) {
   p = __builtin_fma(p, r, 1.0);
   p = __builtin_fma(p, r, 1.0);
   const int ki = (int)k;
-  const double t = tab[kBm64ExpOff + lds_ab<1>((uint32_t)ki & 63u)];
-  return __builtin_ldexp(t * p, ki >> 6);
+  return ExpPre{p, tab[kBm64ExpOff + lds_ab<1>((uint32_t)ki & 63u)], ki};
+}
+__device__ __forceinline__ double exp_tab_fin(const ExpPre &e) {
+  return __builtin_ldexp(e.t * e.p, e.ki >> 6);
+}
+__device__ __forceinline__ double exp_tab(double y, const double *tab) {
+  return exp_tab_fin(exp_tab_pre(y, tab));
 }
 
 // Production log / exp of a ufun dimension (x' = exp(log x + delta)) from the

@@ -2365,11 +2365,11 @@ void mh_gmm_quad_kernel(KArgs a) {
   PBH_PHASE(1);
 
   const int64_t gend = a.g0 + a.n_steps;
-  // FULL: lane p < D writes dim p's record row, the others nothing (the
-  // buffer range check: no select of the dim, no branch)
-  uint32_t xoffm[D];
+  // FULL: lane p writes the group's record row 4 G + p, every dim (the
+  // states staged in LDS for the records), one store per dim per group
+  uint32_t xoffd[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) xoffm[i] = p == i ? (uint32_t)(((int64_t)i * a.n + cc) * 8) : kNoStore;
+  for (int i = 0; i < D; ++i) xoffd[i] = (uint32_t)(((int64_t)i * a.n + cc) * 8);
   const uint32_t rbytes = (uint32_t)(rstride * 8);
   // FULL: the draws are software-pipelined by group -- group G + 1's Philox
   // block(s) are computed beside group G's first step and its Box-Muller
@@ -2377,7 +2377,23 @@ void mh_gmm_quad_kernel(KArgs a) {
   constexpr int NP = (D + 1) / 2, NW = 3 * NP + 1, NB = (NW + 3) / 4;
   double rnext[D];
   uint32_t lnext = 0;
-  if constexpr (FULL) lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
+  // FULL: the step's two filter thresholds, margins folded in, as one packed
+  // pair (thi x 1.000008, tlo x 0.999992): af = thi' ls32 <= E32, rf = tlo'
+  // ls32 > E32 -- one v_pk_mul_f32 per step for the four products of
+  // thi ls32 <= E32 x 0.999992 and tlo ls32 > E32 x 1.000008 (the margin
+  // moves by one fp32 rounding, 7.99e-6 -> 7.87e-6, against the 2.3e-6 error
+  // budget of accept_filter_ms32)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  auto thr_pair = [](uint32_t lead) {
+    constexpr float w = 1.0f / (float)(1u << LB);
+    const float tlo = (float)lead * w;   // exact: lead < 2^24
+    return f32x2{(tlo + w) * 1.000008f, tlo * 0.999992f};
+  };
+  f32x2 thnext = {0.f, 0.f};
+  if constexpr (FULL) {
+    lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
+    thnext = thr_pair(lnext);
+  }
   PBH_PHASE(2);
   const uint32_t slot = FULL && a.fair ? simd_wave_slot() : 0u;
   if constexpr (FULL) {
@@ -2391,8 +2407,13 @@ void mh_gmm_quad_kernel(KArgs a) {
     // component's term, M = max, S = (e0 + e1) + (e2 + e3), M + ln S: the same
     // operations on the same values as the general form's per-step (M, S),
     // so the same bits -- or lp0 while no step of this launch has accepted.
-    // Decisions are the fp64 ratio form's (filter with a 8e-6 margin, the
+    // Decisions are the fp64 ratio form's (filter with a 7.9e-6 margin, the
     // exact form for the rest): |y| <= 40 (log2) on every fp32 weight used.
+    // Measured and not kept: the draws handed to the quad through
+    // LDS instead of DPP broadcasts (+12 %: the reads' latency lands on the
+    // decision chain), and a reference moved by whole powers of two with the
+    // records one group behind, interleaved with the next group's steps (+6 %:
+    // SGPR spills, no gain in issue).
     __shared__ double s_xs[4 * D * kBlock];   // the state after each step
     double kcw[4], kc0[4], kcmw[4][D];          // every component (uniform)
 #pragma unroll
@@ -2404,7 +2425,17 @@ void mh_gmm_quad_kernel(KArgs a) {
       for (int i = 0; i < D; ++i) kcmw[k][i] = ok ? cld(a.tb, k * D + i) * kcw[k] : 0.;
     }
     const double e_absent = exp_tab(-__builtin_inf(), s_bmt);   // exp of a -inf term
-    constexpr float kLw = 1.0f / (float)(1u << LB);
+    // the decision's weight 2^y, y = (v' - R) log2 e, with log2 e folded into
+    // this lane's component constants: y = c0l - sum_i (x'_i cwl - cmwl_i)^2,
+    // cwl = cw sqrt(log2 e), cmwl = cmw sqrt(log2 e), c0l = (c0 - R) log2 e
+    // (per group); two fp64 operations fewer per step.  The fp64 rounding of
+    // the rescaled constants (~1e-16 relative) is far below the argument's
+    // fp32 rounding (4.2e-8 |y|) that the filter's margin covers.
+    constexpr double kSqrtLog2e = 1.2011224087864498;
+    const double cwl = cw * kSqrtLog2e;
+    double cmwl[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) cmwl[i] = cmw[i] * kSqrtLog2e;
     constexpr uint64_t kQ0 = 0x1111111111111111ull;
     double R = lp0;          // the decision's reference (group start)
     uint64_t initm = ~0ull;  // lanes whose chain has not accepted in this launch
@@ -2414,16 +2445,18 @@ void mh_gmm_quad_kernel(KArgs a) {
     // accept words: lane c < 16 reads lane 4 c (chain c of the wave); act16 =
     // the wave's active chains as the word's bits
     const int bperm4 = (lane & 15) * 16;
+    const uint32_t woff = (uint32_t)(wave * 2 + (int64_t)(lane & 3) * a.W * 8);   // step lane & 3's word
     const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);   // SGPRs stay free
     const uint64_t act16 = __ballot(lane < 16 && wave * 16 + lane < a.n);
     for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
       if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
       PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
+      const uint32_t lown = lnext;
       double rown[D];
 #pragma unroll
       for (int i = 0; i < D; ++i) rown[i] = rnext[i];
-      const uint32_t lown = lnext;
-      const float tlown = (float)lown * kLw;
+      const f32x2 thown = thnext;
+      const double c0l = (c0 - R) * 1.4426950408889634;
       uint32_t wn[4 * NB];   // group G + 1's words
       auto next_blocks = [&]() {
 #pragma unroll
@@ -2444,6 +2477,7 @@ void mh_gmm_quad_kernel(KArgs a) {
           if (2 * q + 1 < D) rnext[2 * q + 1] = z1;
         }
         lnext = wn[3 * NP] >> (32 - kStepLead);
+        thnext = thr_pair(lnext);
       };
       double *const gtx = wave_uniform(txrow);
       uint16_t *const gacc = wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W));
@@ -2470,28 +2504,27 @@ void mh_gmm_quad_kernel(KArgs a) {
         double r[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
+        const f32x2 th = {qperm_f32<j * 85>(thown.x), qperm_f32<j * 85>(thown.y)};
         const int64_t g = 4 * G + j;
         double xp[D];
 #pragma unroll
         for (int i = 0; i < D; ++i)
           xp[i] = LOC0 ? __builtin_fma(r[i], psc[i], x[i]) : x[i] + __builtin_fma(r[i], psc[i], plc[i]);
-        const double v = term(xp, cw, c0, cmw);
-        float e32 = __builtin_amdgcn_exp2f((float)((v - R) * 1.4426950408889634));
+        float e32 = __builtin_amdgcn_exp2f((float)term(xp, cwl, c0l, cmwl));
         e32 = e32 + qperm_add_f32<kQuadXor1>(e32);
         const float E32 = e32 + qperm_add_f32<kQuadXor2>(e32);
-        const float tlo = qperm_f32<j * 85>(tlown);
-        const float thi = tlo + kLw;
+        const f32x2 tl = th * ls32;   // (thi' ls32, tlo' ls32)
         // two compares straight into masks (a ballot of their AND would
         // materialise the bool in a VGPR first)
         const uint64_t pinm = __ballot(E32 >= 0x1p-40f) & __ballot(E32 <= 0x1p40f);
         const uint64_t inrm = rinm & sinm & pinm;
-        const uint64_t af = __ballot(thi * ls32 <= E32 * 0.999992f);
-        const uint64_t rf = __ballot(tlo * ls32 > E32 * 1.000008f);
+        const uint64_t af = __ballot(tl.x <= E32);
+        const uint64_t rf = __ballot(tl.y > E32);
         uint64_t accm = inrm & af;
         const uint64_t needm = ~(inrm & (af | rf)) & allm;
         if (needm) {   // wave-uniform, rare: the exact ratio form in fp64
           double M, S, ms_, ss_;
-          quad_ms(v, M, S);                            // the proposal
+          quad_ms(term(xp, cw, c0, cmw), M, S);        // the proposal
           quad_ms(term(x, cw, c0, cmw), ms_, ss_);     // the state
           const bool st0 = __builtin_amdgcn_inverse_ballot_w64(initm);
           const double lm_ = st0 ? lp0 : ms_, ls_ = st0 ? 1.0 : ss_;
@@ -2517,10 +2550,7 @@ void mh_gmm_quad_kernel(KArgs a) {
           mq = __builtin_fma(xo, xo, mq);
         }
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-          st_buf_n(gtx + j * rstride, rbytes, xoffm[i], x[i]);
-          s_xs[(j * D + i) * kBlock + threadIdx.x] = x[i];
-        }
+        for (int i = 0; i < D; ++i) s_xs[(j * D + i) * kBlock + threadIdx.x] = x[i];
         gacm[j] = accm;
       };
       next_blocks();
@@ -2539,26 +2569,37 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int j = 0; j < 4; ++j)
           vf |= __builtin_amdgcn_inverse_ballot_w64(gacm[j]) ? (1u << j) : 0u;
         const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute(bperm4, (int)vf);
+        // lane j < 4 holds step j's word (v_writelane) and one store writes
+        // the four records' words (a store instruction costs more than its
+        // few VALU: one per group instead of one per step)
+        uint32_t wv = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint16_t w16 = (uint16_t)(__ballot((fl >> j) & 1u) & act16);
-          // every lane stores the wave's word (one address, one value)
-          st_buf16(gacc, (uint32_t)(wave * 2), (uint32_t)(j * a.W * 8), w16);
+          const uint32_t w16 = (uint32_t)(__ballot((fl >> j) & 1u) & act16);
+          asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(wv) : "s"(w16), "n"(j));
         }
+        if (lane < 4) st_buf16(gacc, woff, (uint16_t)wv);
       }
-      // ---- the group's records: lane p, the state after step 4 G + p ----
+      // ---- the group's records: lane p, the state after step 4 G + p; its
+      // x rows too (one store per dim per group instead of one per step) ----
       double xs[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) xs[i] = s_xs[(p * D + i) * kBlock + threadIdx.x];
+      for (int i = 0; i < D; ++i) {
+        xs[i] = s_xs[(p * D + i) * kBlock + threadIdx.x];
+        st_buf_n(gtx, 4 * rbytes, (uint32_t)p * rbytes + xoffd[i], xs[i]);   // row 4 G + p
+      }
       const uint64_t pinit = (ginit[0] & kQ0) | (ginit[1] & (kQ0 << 1)) |
                              (ginit[2] & (kQ0 << 2)) | (ginit[3] & (kQ0 << 3));
       double vk[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) vk[k] = k < K ? term(xs, kcw[k], kc0[k], kcmw[k]) : -__builtin_inf();
       const double M = max_f64_raw(max_f64_raw(vk[0], vk[1]), max_f64_raw(vk[2], vk[3]));
+      ExpPre ep[4];
+#pragma unroll
+      for (int k = 0; k < K; ++k) ep[k] = exp_tab_pre(vk[k] - M, s_bmt);   // the K table reads first
       double ek[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) ek[k] = k < K ? exp_tab(vk[k] - M, s_bmt) : e_absent;
+      for (int k = 0; k < 4; ++k) ek[k] = k < K ? exp_tab_fin(ep[k]) : e_absent;
       const double S = (ek[0] + ek[1]) + (ek[2] + ek[3]);
       const bool pi0 = __builtin_amdgcn_inverse_ballot_w64(pinit);
       const double pm = pi0 ? lp0 : M, pss = pi0 ? 1.0 : S;
