@@ -191,9 +191,13 @@ def load():
   return lib
 
 
+def raise_status(name, rc):
+  raise PbhError(name, rc, load().pbh_last_error().decode())
+
+
 def call(name, *args):
   lib = load()
   rc = getattr(lib, name)(*args)
   if rc != 0:
-    raise PbhError(name, rc, lib.pbh_last_error().decode())
+    raise_status(name, rc)
   return rc

@@ -1503,7 +1503,6 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
 
 int pbh_sync(pbh_engine *e) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
-  HIP_TRY(hipSetDevice(e->device));
   if (e->srv_active) {   // never the stream: the server kernel is on it
     if (e->srv_pending) {
       const int rc = srv_wait(e, e->srv_pending, false);
@@ -1513,6 +1512,7 @@ int pbh_sync(pbh_engine *e) {
     }
     return PBH_OK;
   }
+  HIP_TRY(hipSetDevice(e->device));
   if (e->spin_sync) {
     // poll the stream for up to 2 ms: a short launch's completion is seen
     // within a microsecond or so (a blocking wait sleeps on the completion

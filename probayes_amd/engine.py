@@ -103,6 +103,10 @@ class Engine:
     self.dim = self.spec['dim']
     self._h = _c.c_void_p()
     _lib.call('pbh_create', int(device), _c.byref(self._h))
+    # the hot entry points, bound once (the timed run is two calls: a
+    # getattr and c_int64 boxing per call were ~1 us of a 20-step run's ~35)
+    lib = _lib.load()
+    self._fn_run, self._fn_sync = lib.pbh_run, lib.pbh_sync
     _LIVE.add(self)
     self.device = device
     self.n = 0
@@ -284,8 +288,9 @@ class Engine:
     self.debug = bool(debug)
 
   def run(self, n_steps, steps_per_launch=0, sync=True):
-    _lib.call('pbh_run', self._h, _c.c_int64(int(n_steps)),
-              int(steps_per_launch))
+    rc = self._fn_run(self._h, int(n_steps), int(steps_per_launch))
+    if rc:
+      _lib.raise_status('pbh_run', rc)
     if sync:
       self.sync()
 
@@ -299,7 +304,9 @@ class Engine:
       self.sync()
 
   def sync(self):
-    _lib.call('pbh_sync', self._h)
+    rc = self._fn_sync(self._h)
+    if rc:
+      _lib.raise_status('pbh_sync', rc)
 
   def set_collect(self, moments=True):
     """moments=False: the kernels keep no running moments (no per-launch
