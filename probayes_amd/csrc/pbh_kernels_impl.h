@@ -2305,7 +2305,8 @@ __device__ __attribute__((noinline)) bool gmm_quad_exact(
   return ratio_accept(lpp * acc_beta, lpc * acc_beta, t, false, log_npi);
 }
 
-// FULL: the steady-state launch (gmm_quad_full): whole groups of 4 steps,
+// FULL: the steady-state launch (gmm_quad_full): whole groups of GS = 8
+// steps where the launch's start and length are multiples of 8, else of 4,
 // every step recorded (thin 1, inside the trace), the chains past step 1 and
 // the plain ratio form (acc_beta = 1) -- no per-step range, record or
 // first-step tests, and branch-free stores: a lane with nothing of its own
@@ -2317,9 +2318,11 @@ __device__ __attribute__((noinline)) bool gmm_quad_exact(
 // (test_gmm_quad_steady_state_form_is_the_general_form).
 // LOC0: every proposal loc is 0 (the examples' norm.rvs(scale=...)): x' =
 // fma(r, scale, x), one rounding, instead of x + fma(r, scale, loc).
-template <int D, int K, bool MOM, bool FULL, bool LOC0 = false>
+template <int D, int K, bool MOM, bool FULL, bool LOC0 = false, int GS = 4>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
 void mh_gmm_quad_kernel(KArgs a) {
+  static_assert(GS == 4 || GS == 8, "quad kernel: groups of 4 or 8 steps");
+  static_assert(GS == 4 || FULL, "the general form runs groups of 4");
   static_assert(K >= 1 && K <= 4 && D >= 1 && D <= 4, "quad kernel: K, D <= 4");
   constexpr int LB = kStepLead;          // threshold lead bits (step_draws)
   __shared__ double s_bmt[kBm64Doubles];
@@ -2375,8 +2378,9 @@ void mh_gmm_quad_kernel(KArgs a) {
   // block(s) are computed beside group G's first step and its Box-Muller
   // pair(s) beside the second (step_draws' words and arithmetic, split)
   constexpr int NP = (D + 1) / 2, NW = 3 * NP + 1, NB = (NW + 3) / 4;
-  double rnext[D];
-  uint32_t lnext = 0;
+  constexpr int NG = GS / 4;   // draw sets per lane per group (FULL)
+  double rnext[NG][D];
+  uint32_t lnext[NG] = {};
   // FULL: the step's two filter thresholds, margins folded in, as one packed
   // pair (thi x 1.000008, tlo x 0.999992): af = thi' ls32 <= E32, rf = tlo'
   // ls32 > E32 -- one v_pk_mul_f32 per step for the four products of
@@ -2389,10 +2393,13 @@ void mh_gmm_quad_kernel(KArgs a) {
     const float tlo = (float)lead * w;   // exact: lead < 2^24
     return f32x2{(tlo + w) * 1.000008f, tlo * 0.999992f};
   };
-  f32x2 thnext = {0.f, 0.f};
+  f32x2 thnext[NG];
   if constexpr (FULL) {
-    lnext = step_draws<D>(a, 4 * (a.g0 >> 2) + p, chain, s_bmt, rnext);
-    thnext = thr_pair(lnext);
+#pragma unroll
+    for (int h = 0; h < NG; ++h) {
+      lnext[h] = step_draws<D>(a, a.g0 + 4 * h + p, chain, s_bmt, rnext[h]);   // g0 % GS == 0
+      thnext[h] = thr_pair(lnext[h]);
+    }
   }
   PBH_PHASE(2);
   const uint32_t slot = FULL && a.fair ? simd_wave_slot() : 0u;
@@ -2414,7 +2421,11 @@ void mh_gmm_quad_kernel(KArgs a) {
     // decision chain), and a reference moved by whole powers of two with the
     // records one group behind, interleaved with the next group's steps (+6 %:
     // SGPR spills, no gain in issue).
-    __shared__ double s_xs[4 * D * kBlock];   // the state after each step
+    // GS = 8: groups of eight steps, lane p drawing steps GS G + p and GS G +
+    // 4 + p and recording the states after them: the per-group work (the
+    // reference's re-anchoring, the accept words' assembly and store, the
+    // loop and priority bookkeeping) is paid once per eight steps
+    __shared__ double s_xs[GS * D * kBlock];   // the state after each step
     double kcw[4], kc0[4], kcmw[4][D];          // every component (uniform)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2445,43 +2456,50 @@ void mh_gmm_quad_kernel(KArgs a) {
     // accept words: lane c < 16 reads lane 4 c (chain c of the wave); act16 =
     // the wave's active chains as the word's bits
     const int bperm4 = (lane & 15) * 16;
-    const uint32_t woff = (uint32_t)(wave * 2 + (int64_t)(lane & 3) * a.W * 8);   // step lane & 3's word
+    const uint32_t woff = (uint32_t)(wave * 2 + (int64_t)(lane & (GS - 1)) * a.W * 8);   // step lane's word
     const PhiloxKeys rk = philox_keys_v(a.seed_lo, a.seed_hi);   // SGPRs stay free
     const uint64_t act16 = __ballot(lane < 16 && wave * 16 + lane < a.n);
-    for (int64_t G = a.g0 >> 2; G * 4 < gend; ++G) {
+    for (int64_t G = a.g0 / GS; G * GS < gend; ++G) {
       if (a.fair) fair_prio((uint32_t)(__builtin_amdgcn_s_memrealtime() >> a.fair) + slot);
-      PBH_PHASE_Q(G - (a.g0 >> 2), (gend + 3) / 4 - (a.g0 >> 2));
-      const uint32_t lown = lnext;
-      double rown[D];
+      PBH_PHASE_Q(G - a.g0 / GS, (gend + GS - 1) / GS - a.g0 / GS);
+      uint32_t lown[NG];
+      double rown[NG][D];
+      f32x2 thown[NG];
 #pragma unroll
-      for (int i = 0; i < D; ++i) rown[i] = rnext[i];
-      const f32x2 thown = thnext;
+      for (int h = 0; h < NG; ++h) {
+        lown[h] = lnext[h];
+        thown[h] = thnext[h];
+#pragma unroll
+        for (int i = 0; i < D; ++i) rown[h][i] = rnext[h][i];
+      }
       const double c0l = (c0 - R) * 1.4426950408889634;
-      uint32_t wn[4 * NB];   // group G + 1's words
-      auto next_blocks = [&]() {
+      uint32_t wn[NG][4 * NB];   // group G + 1's words
+      auto next_blocks = [&](auto H_) {
+        constexpr int h = decltype(H_)::value;
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const u32x4 b = philox4x32_10_rk(ctr(q, 4 * (G + 1) + p, chain), rk);
-          wn[4 * q] = b.x;
-          wn[4 * q + 1] = b.y;
-          wn[4 * q + 2] = b.z;
-          wn[4 * q + 3] = b.w;
+          const u32x4 b = philox4x32_10_rk(ctr(q, GS * (G + 1) + 4 * h + p, chain), rk);
+          wn[h][4 * q] = b.x;
+          wn[h][4 * q + 1] = b.y;
+          wn[h][4 * q + 2] = b.z;
+          wn[h][4 * q + 3] = b.w;
         }
       };
-      auto next_normals = [&]() {
+      auto next_normals = [&](auto H_) {
+        constexpr int h = decltype(H_)::value;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
           double z0, z1;
-          bm96_pair(wn[3 * q], wn[3 * q + 1], wn[3 * q + 2], s_bmt, z0, z1);
-          rnext[2 * q] = z0;
-          if (2 * q + 1 < D) rnext[2 * q + 1] = z1;
+          bm96_pair(wn[h][3 * q], wn[h][3 * q + 1], wn[h][3 * q + 2], s_bmt, z0, z1);
+          rnext[h][2 * q] = z0;
+          if (2 * q + 1 < D) rnext[h][2 * q + 1] = z1;
         }
-        lnext = wn[3 * NP] >> (32 - kStepLead);
-        thnext = thr_pair(lnext);
+        lnext[h] = wn[h][3 * NP] >> (32 - kStepLead);
+        thnext[h] = thr_pair(lnext[h]);
       };
       double *const gtx = wave_uniform(txrow);
       uint16_t *const gacc = wave_uniform(reinterpret_cast<uint16_t *>(a.tacc + ri * a.W));
-      uint64_t ginit[4], gacm[4];
+      uint64_t ginit[GS], gacm[GS];
       // the quad's (M, S) of a term v (the general form's record arithmetic)
       auto quad_ms = [&](double v, double &M, double &S) {
         M = max_f64_raw(v, qperm_f64<kQuadXor1>(v));
@@ -2500,12 +2518,12 @@ void mh_gmm_quad_kernel(KArgs a) {
         return v;
       };
       auto step = [&](auto J) {
-        constexpr int j = decltype(J)::value;
+        constexpr int j = decltype(J)::value, h = j / 4, jq = j % 4;   // set h, lane jq's draws
         double r[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) r[i] = qperm_f64<j * 85>(rown[i]);
-        const f32x2 th = {qperm_f32<j * 85>(thown.x), qperm_f32<j * 85>(thown.y)};
-        const int64_t g = 4 * G + j;
+        for (int i = 0; i < D; ++i) r[i] = qperm_f64<jq * 85>(rown[h][i]);
+        const f32x2 th = {qperm_f32<jq * 85>(thown[h].x), qperm_f32<jq * 85>(thown[h].y)};
+        const int64_t g = GS * G + j;
         double xp[D];
 #pragma unroll
         for (int i = 0; i < D; ++i)
@@ -2528,7 +2546,7 @@ void mh_gmm_quad_kernel(KArgs a) {
           quad_ms(term(x, cw, c0, cmw), ms_, ss_);     // the state
           const bool st0 = __builtin_amdgcn_inverse_ballot_w64(initm);
           const double lm_ = st0 ? lp0 : ms_, ls_ = st0 ? 1.0 : ss_;
-          const uint32_t ld = qperm_u32<j * 85>(lown);
+          const uint32_t ld = qperm_u32<jq * 85>(lown[h]);
           bool ex = false;
           if (__builtin_amdgcn_inverse_ballot_w64(needm))
             ex = gmm_quad_exact(a.seed_lo, a.seed_hi, a.acc_beta, a.log_npi, s_bmt,
@@ -2553,67 +2571,83 @@ void mh_gmm_quad_kernel(KArgs a) {
         for (int i = 0; i < D; ++i) s_xs[(j * D + i) * kBlock + threadIdx.x] = x[i];
         gacm[j] = accm;
       };
-      next_blocks();
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      next_blocks(I0{});
       step(std::integral_constant<int, 0>{});
-      next_normals();
+      next_normals(I0{});
       step(std::integral_constant<int, 1>{});
+      if constexpr (NG == 2) next_blocks(I1{});
       step(std::integral_constant<int, 2>{});
+      if constexpr (NG == 2) next_normals(I1{});
       step(std::integral_constant<int, 3>{});
+      if constexpr (GS == 8) {
+        step(std::integral_constant<int, 4>{});
+        step(std::integral_constant<int, 5>{});
+        step(std::integral_constant<int, 6>{});
+        step(std::integral_constant<int, 7>{});
+      }
       {
-        // the group's accept words: lane c < 16 takes chain c's four decision
+        // the group's accept words: lane c < 16 takes chain c's GS decision
         // bits from its quad (lane 4 c, ds_bpermute) and each step's word is
         // one ballot -- instead of compressing every step's 64-bit mask on
         // the SALU
         uint32_t vf = 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < GS; ++j)
           vf |= __builtin_amdgcn_inverse_ballot_w64(gacm[j]) ? (1u << j) : 0u;
         const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute(bperm4, (int)vf);
-        // lane j < 4 holds step j's word (v_writelane) and one store writes
-        // the four records' words (a store instruction costs more than its
-        // few VALU: one per group instead of one per step)
+        // lane j < GS holds step j's word (v_writelane) and one store writes
+        // the group's words (a store instruction costs more than its few
+        // VALU: one per group instead of one per step)
         uint32_t wv = 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < GS; ++j) {
           const uint32_t w16 = (uint32_t)(__ballot((fl >> j) & 1u) & act16);
           asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(wv) : "s"(w16), "n"(j));
         }
-        if (lane < 4) st_buf16(gacc, woff, (uint16_t)wv);
+        if (lane < GS) st_buf16(gacc, woff, (uint16_t)wv);
       }
-      // ---- the group's records: lane p, the state after step 4 G + p; its
-      // x rows too (one store per dim per group instead of one per step) ----
-      double xs[D];
+      // ---- the group's records: lane p, the states after steps GS G + 4 h
+      // + p; their x rows too (one store per dim and state per group instead
+      // of one per dim per step) ----
+      double pm = lp0, pss = 1.0;
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        xs[i] = s_xs[(p * D + i) * kBlock + threadIdx.x];
-        st_buf_n(gtx, 4 * rbytes, (uint32_t)p * rbytes + xoffd[i], xs[i]);   // row 4 G + p
+      for (int h = 0; h < NG; ++h) {
+        double xs[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          xs[i] = s_xs[((4 * h + p) * D + i) * kBlock + threadIdx.x];
+          st_buf_n(gtx, GS * rbytes, (uint32_t)(4 * h + p) * rbytes + xoffd[i], xs[i]);   // row GS G + 4 h + p
+        }
+        const uint64_t pinit = (ginit[4 * h] & kQ0) | (ginit[4 * h + 1] & (kQ0 << 1)) |
+                               (ginit[4 * h + 2] & (kQ0 << 2)) | (ginit[4 * h + 3] & (kQ0 << 3));
+        double vk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vk[k] = k < K ? term(xs, kcw[k], kc0[k], kcmw[k]) : -__builtin_inf();
+        const double M = max_f64_raw(max_f64_raw(vk[0], vk[1]), max_f64_raw(vk[2], vk[3]));
+        ExpPre ep[4];
+#pragma unroll
+        for (int k = 0; k < K; ++k) ep[k] = exp_tab_pre(vk[k] - M, s_bmt);   // the K table reads first
+        double ek[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ek[k] = k < K ? exp_tab_fin(ep[k]) : e_absent;
+        const double S = (ek[0] + ek[1]) + (ek[2] + ek[3]);
+        const bool pi0 = __builtin_amdgcn_inverse_ballot_w64(pinit);
+        pm = pi0 ? lp0 : M;
+        pss = pi0 ? 1.0 : S;
+        const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
+        st_buf(wave_uniform(a.tlp + (ri + 4 * h) * a.n), lpoff, 0, lpr);
       }
-      const uint64_t pinit = (ginit[0] & kQ0) | (ginit[1] & (kQ0 << 1)) |
-                             (ginit[2] & (kQ0 << 2)) | (ginit[3] & (kQ0 << 3));
-      double vk[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) vk[k] = k < K ? term(xs, kcw[k], kc0[k], kcmw[k]) : -__builtin_inf();
-      const double M = max_f64_raw(max_f64_raw(vk[0], vk[1]), max_f64_raw(vk[2], vk[3]));
-      ExpPre ep[4];
-#pragma unroll
-      for (int k = 0; k < K; ++k) ep[k] = exp_tab_pre(vk[k] - M, s_bmt);   // the K table reads first
-      double ek[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ek[k] = k < K ? exp_tab_fin(ep[k]) : e_absent;
-      const double S = (ek[0] + ek[1]) + (ek[2] + ek[3]);
-      const bool pi0 = __builtin_amdgcn_inverse_ballot_w64(pinit);
-      const double pm = pi0 ? lp0 : M, pss = pi0 ? 1.0 : S;
-      const double lpr = pm == lp0 && pss == 1.0 ? lp0 : pm + ln_tab(pss, s_bmt);
-      st_buf(wave_uniform(a.tlp + ri * a.n), lpoff, 0, lpr);
-      // the next group's reference: the state after step 4 G + 3 (lane 3)
+      // the next group's reference: the state after step GS G + GS - 1 (lane 3)
       R = qbcast_f64<3>(pm);
       lm = R;
       ls = qbcast_f64<3>(pss);
       ls32 = (float)ls;
       rinm = __ballot(__builtin_fabs(R) <= 650.);
       sinm = allm;   // ls in [1, K] (or 1)
-      ri += 4;
-      txrow += 4 * rstride;
+      ri += GS;
+      txrow += GS * rstride;
     }
   } else {
   // ---- the general form: any launch (partial groups, thinning, step 1,
@@ -3478,7 +3512,7 @@ inline bool gmm_pair_form(const KArgs &a) {
 }
 
 // The quad kernel's steady-state form applies (see mh_gmm_quad_kernel FULL):
-// whole 4-step groups, thin 1, every record inside the trace, past step 1,
+// whole 4-step groups (8-step ones where gmm_quad_full8), thin 1, every record inside the trace, past step 1,
 // acc_beta = 1.  PBH_GMM_FULL=0 (engine: gmm_full) keeps the general form.
 inline bool gmm_quad_full(const KArgs &a) {
   return a.gmm_full && a.has_pred && a.acc_beta == 1.0 && a.thin == 1 &&
@@ -3488,26 +3522,44 @@ inline bool gmm_quad_full(const KArgs &a) {
          a.g0 - a.rec_base >= 0 && a.g0 + a.n_steps - a.rec_base <= a.rec_cap;
 }
 
+// FULL groups of eight steps where the launch allows (g0 and n_steps
+// multiples of 8, eight record rows addressable), else of four
+inline bool gmm_quad_full8(const KArgs &a) {
+  return a.g0 % 8 == 0 && a.n_steps % 8 == 0 &&
+         (int64_t)8 * a.d * a.n * 8 < (int64_t(1) << 32);
+}
+
+template <int D, int K, bool MOM, bool FULL, bool LOC0>
+void launch_gmm_quad_k(const KArgs &a, const dim3 &grid, const dim3 &block, hipStream_t st) {
+  if constexpr (FULL) {
+    if (gmm_quad_full8(a)) {
+      pbh_launch((mh_gmm_quad_kernel<D, K, MOM, true, LOC0, 8>), grid, block, 0, st, a);
+      return;
+    }
+  }
+  pbh_launch((mh_gmm_quad_kernel<D, K, MOM, FULL, LOC0>), grid, block, 0, st, a);
+}
+
 template <int D, bool MOM, bool FULL>
 void launch_gmm_quad(const KArgs &a, const dim3 &grid, const dim3 &block,
                      hipStream_t st) {
   if constexpr (D == 2) {   // cfg5's d: the zero-loc form
     if (a.ploc_zero) {
       if (a.tn == 2)
-        pbh_launch((mh_gmm_quad_kernel<D, 2, MOM, FULL, true>), grid, block, 0, st, a);
+        launch_gmm_quad_k<D, 2, MOM, FULL, true>(a, grid, block, st);
       else if (a.tn == 3)
-        pbh_launch((mh_gmm_quad_kernel<D, 3, MOM, FULL, true>), grid, block, 0, st, a);
+        launch_gmm_quad_k<D, 3, MOM, FULL, true>(a, grid, block, st);
       else
-        pbh_launch((mh_gmm_quad_kernel<D, 4, MOM, FULL, true>), grid, block, 0, st, a);
+        launch_gmm_quad_k<D, 4, MOM, FULL, true>(a, grid, block, st);
       return;
     }
   }
   if (a.tn == 2)
-    pbh_launch((mh_gmm_quad_kernel<D, 2, MOM, FULL>), grid, block, 0, st, a);
+    launch_gmm_quad_k<D, 2, MOM, FULL, false>(a, grid, block, st);
   else if (a.tn == 3)
-    pbh_launch((mh_gmm_quad_kernel<D, 3, MOM, FULL>), grid, block, 0, st, a);
+    launch_gmm_quad_k<D, 3, MOM, FULL, false>(a, grid, block, st);
   else
-    pbh_launch((mh_gmm_quad_kernel<D, 4, MOM, FULL>), grid, block, 0, st, a);
+    launch_gmm_quad_k<D, 4, MOM, FULL, false>(a, grid, block, st);
 }
 
 template <int D>

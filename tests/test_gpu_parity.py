@@ -472,11 +472,14 @@ def test_gmm_lane_pair_kernel_matches_one_lane_kernel(monkeypatch, lanes):
   np.testing.assert_allclose(mp['sum'], m1['sum'], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize('spl', [64, 20])
 @pytest.mark.parametrize('mom', [True, False])
-def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
-  """The quad kernel's steady-state launch (whole 4-step groups, no
-  per-step range / record tests, branch-free stores) is bit-for-bit the
-  general form (PBH_GMM_FULL=0); ragged chain count, several launches."""
+def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom, spl):
+  """The quad kernel's steady-state launch (whole groups of 8 steps where
+  the launch's start and length allow -- 64-step launches -- else of 4 --
+  20-step launches; no per-step range / record tests, branch-free stores) is
+  bit-for-bit the general form (PBH_GMM_FULL=0); ragged chain count,
+  several launches."""
   from probayes_amd import Engine
   spec = oracle.golden_spec('gmm2')
   n, t = 3000 + 5, 200
@@ -488,7 +491,7 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom):
     eng.set_rng('philox', seed=9)
     eng.set_collect(moments=mom)
     eng.alloc_trace(t, 1)
-    eng.run(t, steps_per_launch=64)
+    eng.run(t, steps_per_launch=spl)
     outs[full] = (eng.trace(), eng.moments() if mom else None, eng.state())
     eng.close()
   (ta, ma, sa), (tb, mb, sb) = outs['1'], outs['0']
