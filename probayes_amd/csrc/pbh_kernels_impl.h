@@ -2426,14 +2426,16 @@ void mh_gmm_quad_kernel(KArgs a) {
     // reference's re-anchoring, the accept words' assembly and store, the
     // loop and priority bookkeeping) is paid once per eight steps
     __shared__ double s_xs[GS * D * kBlock];   // the state after each step
-    double kcw[4], kc0[4], kcmw[4][D];          // every component (uniform)
+    // every component's constants (uniform; held in VGPRs -- in SGPRs they
+    // pushed ~30 SGPR spill reloads per group into the loop)
+    double kcw[4], kc0[4], kcmw[4][D];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool ok = k < K;
-      kcw[k] = ok ? cld(a.tw, k) : 0.;
-      kc0[k] = ok ? cld(a.tw, K + k) : -__builtin_inf();
+      kcw[k] = ok ? in_vgpr_f64(cld(a.tw, k)) : 0.;
+      kc0[k] = ok ? in_vgpr_f64(cld(a.tw, K + k)) : -__builtin_inf();
 #pragma unroll
-      for (int i = 0; i < D; ++i) kcmw[k][i] = ok ? cld(a.tb, k * D + i) * kcw[k] : 0.;
+      for (int i = 0; i < D; ++i) kcmw[k][i] = ok ? in_vgpr_f64(cld(a.tb, k * D + i) * kcw[k]) : 0.;
     }
     const double e_absent = exp_tab(-__builtin_inf(), s_bmt);   // exp of a -inf term
     // the decision's weight 2^y, y = (v' - R) log2 e, with log2 e folded into
