@@ -503,6 +503,37 @@ def test_gmm_quad_steady_state_form_is_the_general_form(monkeypatch, mom, spl):
       assert np.array_equal(ma[k], mb[k]), k
 
 
+def test_gmm_quad_full_size_cfg5_is_the_general_form(monkeypatch):
+  """cfg5's per-GPU share at full size -- 32 768 chains, an 8-step warm-up,
+  then one 2 000-step launch (the steady-state form in 8-step groups) --
+  equals the general form (PBH_GMM_FULL=0) bit for bit: the final state and
+  the device reductions of the whole trace (per-chain sums, sums of
+  squares and accept counts, and the recorded v.prob's expectation)."""
+  from probayes_amd import Engine
+  spec = oracle.golden_spec('gmm2')
+  n, t = 32768, 2000
+  outs = {}
+  for full in ('1', '0'):
+    monkeypatch.setenv('PBH_GMM_FULL', full)
+    eng = Engine(spec)
+    eng.init_chains(golden_init('gmm2', n))
+    eng.set_rng('philox', seed=23)
+    eng.set_collect(moments=False)
+    eng.run(8)
+    eng.alloc_trace(t, 1)
+    eng.run(t)
+    st = eng.trace_stats(0, t)
+    ex = eng.trace_expectation(0, t)
+    outs[full] = (eng.state(), st, ex)
+    eng.close()
+  (sa, ta, ea), (sb, tb, eb) = outs['1'], outs['0']
+  assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+  for k in ('sum', 'sumsq', 'n_acc'):
+    assert np.array_equal(ta[k], tb[k]), k
+  assert np.array_equal(ea, eb)
+  assert ta['n_acc'].min() > 0   # every chain moved
+
+
 @pytest.mark.parametrize('pair', ['1', '0'])
 @pytest.mark.parametrize('n', [4096 + 5, 37])
 def test_iid_steady_state_form_is_the_general_form(monkeypatch, pair, n):
