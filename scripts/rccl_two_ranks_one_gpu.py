@@ -10,8 +10,9 @@ model (dist.shard, global chain offsets); the ncclUniqueId travels over TCP
 
 The parent never touches the GPU: it starts the ranks as child processes and
 compares what they wrote.  One process per GPU is the production layout; two
-ranks on one device is a hardware test of the collectives' code path only
-(RCCL may refuse it as a duplicate GPU: that outcome is printed, not hidden).
+ranks on one device would test the collectives' code path only -- and this
+RCCL refuses it: ncclCommInitRank fails with "Duplicate GPU detected" on both
+ranks (profiles/r05s2/rccl_one_card.txt), so world > 1 needs a real node.
 usage: python scripts/rccl_two_ranks_one_gpu.py OUTDIR"""
 import json
 import os
