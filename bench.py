@@ -162,12 +162,15 @@ def lib_sha256():
   return h.hexdigest()
 
 
-def measured_traffic(chains, launch_steps, rng, trace, sha=None):
-  """HBM bytes per launch of this exact launch shape (chains, steps in the
-  launch, RNG mode) measured on THIS library build: the newest
+def measured_traffic(chains, launch_steps, rng, trace, sha=None, srv=False):
+  """HBM bytes per launch (per command when srv) of this exact shape (chains,
+  steps in the launch or command, RNG mode, resident-server instance or
+  launched) measured on THIS library build: the newest
   profiles/r*_traffic*.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
-  scripts/profile_r04.sh + tools/collect_profiles.py) whose lib_sha256 is the
-  loaded library's; None when no profile of this binary matches."""
+  scripts/profile_r06.sh + tools/collect_r06.py) whose lib_sha256 is the
+  loaded library's and whose kernel instance is the one timed (`srv`: the
+  server's one dispatch, its bytes divided over the steps commanded in its
+  life); None when no profile of this binary and instance matches."""
   import glob
   if not trace:
     return None
@@ -178,22 +181,24 @@ def measured_traffic(chains, launch_steps, rng, trace, sha=None):
       t = json.load(f)
     if (t.get('lib_sha256') == sha and
         t.get('kernel', '').startswith('mh_pair_kernel') and
+        bool(t.get('srv', False)) == bool(srv) and
         t.get('chains') == chains and t.get('rng', 'philox_fp32') == rng and
         t.get('steps_per_launch') == launch_steps):
       return t['bytes_per_launch']
   return None
 
 
-def kernel_label(args, n):
+def kernel_label(args, n, srv=False):
   """The kernel the timed launches run (the engine's dispatch rules,
-  pbh_kernels_impl.h launch_mh_pair_m / pair_full_form)."""
+  pbh_kernels_impl.h launch_mh_pair_m / pair_full_form); srv: the timed run
+  was a command to the resident server (its SRV instance)."""
   if os.environ.get('PBH_NO_PAIR'):
     return 'mh_kernel<10, {}, DIAG, GAUSS>'.format(args.rng.upper())
   mom = int(args.moments or args.no_trace)
   full = (args.rng == 'philox' and not mom and n % 32 == 0 and
           os.environ.get('PBH_PAIR_FULL', '1') != '0')
-  return 'mh_pair_kernel<10, {}, MOM={}{}>'.format(args.rng.upper(), mom,
-                                                  ', FULL' if full else '')
+  return 'mh_pair_kernel<10, {}, MOM={}{}{}>'.format(
+      args.rng.upper(), mom, ', FULL' if full else '', ', SRV' if srv else '')
 
 
 class EngineCollective:
@@ -221,7 +226,8 @@ class EngineCollective:
 
 
 def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
-             trace=True, moments=False, seed=20261015, warmup_spl=None):
+             trace=True, moments=False, seed=20261015, warmup_spl=None,
+             gather=True):
   """One rank of the bench (weak scaling: chains_per_gpu chains per rank):
   shard the global chain ids, warm up, time exactly `steps` steps between
   barriers, take the max over ranks, then collect the per-chain statistics
@@ -270,12 +276,42 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
          'launches': launches, 'enqueue_s': t1 - t0, 'server': server}
   if col is not None:
     out['el'] = col.allreduce_max(el)
+    if not gather:
+      return out
     t1 = time.perf_counter()
     if trace and not moments:
       eng.trace_stats(warmup, steps)   # device reduction of the timed steps
     out['stats'] = col.gather_stats()
     out['collect_ms'] = (time.perf_counter() - t1) * 1e3
   return out
+
+
+def run_launched_rank(make_engine, col, rank, world, chains_per_gpu, steps,
+                      warmup, spl, rng, trace, moments, warmup_spl):
+  """The headline's shape with the resident server off (PBH_SERVER=0: every
+  run launches the kernel, the engine's default for SP.sampler users), on a
+  fresh engine, timed the same way (barrier + sync on both sides, max over
+  ranks) after the headline: chain-steps/s of the whole job (not `value`)."""
+  prev = os.environ.get('PBH_SERVER')
+  os.environ['PBH_SERVER'] = '0'   # read at pbh_create
+  try:
+    eng = make_engine()
+  finally:
+    if prev is None:
+      os.environ.pop('PBH_SERVER', None)
+    else:
+      os.environ['PBH_SERVER'] = prev
+  try:
+    res = run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl,
+                   rng, trace=trace, moments=moments, warmup_spl=warmup_spl,
+                   gather=False)
+  finally:
+    eng.close()
+  kern_ms, launches = res['kern_ms'], res['launches']
+  return {'chain_steps_per_s': float(chains_per_gpu) * world * steps / res['el'],
+          'ms_per_step': res['el'] * 1e3 / steps,
+          'events_us': kern_ms * 1e3, 'launches': launches,
+          'host_enqueue_us': res['enqueue_s'] * 1e6}
 
 
 def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup,
@@ -351,6 +387,9 @@ def main():
                   help='HBM bytes per launch from a rocprofv3 PMC pass')
   ap.add_argument('--no-replay', action='store_true',
                   help='skip the reference-identical REPLAY line fields')
+  ap.add_argument('--no-launched', action='store_true',
+                  help='skip the launched-form (PBH_SERVER=0) rate that is '
+                  'reported beside a resident-server headline')
   args = ap.parse_args()
 
   world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -394,6 +433,15 @@ def main():
                  spl, args.rng, trace=not args.no_trace, moments=args.moments,
                  warmup_spl=args.warmup_spl)
   n, el, kern_ms, launches = res['n'], res['el'], res['kern_ms'], res['launches']
+  srv = bool(res.get('server') and res['server'].get('commands'))
+  launched = None
+  if srv and not args.no_launched:
+    # the same shape launched per run (the engine's default form), after the
+    # headline: reported beside value, never folded into it
+    launched = run_launched_rank(lambda: Engine(cfg2_spec(), device=local), col,
+                                 rank, world, args.chains, args.steps,
+                                 args.warmup, spl, args.rng, not args.no_trace,
+                                 args.moments, args.warmup_spl)
   replay = None
   if not args.no_replay:
     # after the headline's timed region and its collection, on a fresh engine
@@ -431,9 +479,9 @@ def main():
                      'traffic': args.traffic_bytes if args.traffic_bytes
                                 else measured_traffic(
                                     n, min(spl, args.steps), args.rng,
-                                    not args.no_trace, sha),
+                                    not args.no_trace, sha, srv=srv),
                      'bytes_per_chain_step': bpcs,
-                     'kernel': kernel_label(args, n),
+                     'kernel': kernel_label(args, n, srv),
                      'avg_launch_ms': avg_launch_s * 1e3,
                      'launches': launches},
         'kernel_chain_steps_per_s': n * args.steps / (kern_ms / 1e3),
@@ -452,6 +500,12 @@ def main():
     }
     if collect_ms is not None:
       line['rccl_allgather_ms'] = collect_ms
+    if launched is not None:
+      # PBH_SERVER=0 on the same shape and clock: what SP.sampler users get
+      line['launched_chain_steps_per_s'] = launched['chain_steps_per_s']
+      line['launched'] = dict(launched, kernel=kernel_label(args, n, False),
+                              note='PBH_SERVER=0, fresh engine, timed after '
+                                   'the headline; not folded into value')
     if replay is not None:
       # the parity mode (reference-identical chains), same shape and clock;
       # reported beside value, never folded into it

@@ -132,7 +132,15 @@ struct pbh_engine {
   pbh::SrvDone *srv_done = nullptr;
   pbh::SrvCmd *srv_mail = nullptr;   // device memory: workgroup 0's relay
   int32_t srv_done_len = 0;
+  // srv_last: the last submit (or launch) -- never moved forward at a wait:
+  // a command completes after its submit, and each workgroup's idle timer
+  // starts at its completion, so idle measured from the submit is an upper
+  // bound on the kernel's own
   std::chrono::steady_clock::time_point srv_last{};
+  // a server command was lost (the kernel ended or hung before completing
+  // it): the chain state may be partly advanced, so runs refuse until
+  // pbh_init_chains / pbh_restore / pbh_set_chains replace it
+  bool state_lost = false;
   int64_t srv_commands = 0, srv_launches = 0;
   // RCCL
   ncclComm_t comm = nullptr;
@@ -263,10 +271,21 @@ int srv_wait(pbh_engine *e, uint32_t seq, bool ok_if_ended) {
       const auto el = srv_clk::now() - t0;
       if (el > std::chrono::milliseconds(1) && srv_kernel_ended(e)) {
         if (srv_all_done(e, seq) || ok_if_ended) return PBH_OK;
-        return fail(PBH_ERR_HIP, "sampling server ended before command %u completed", seq);
+        // the kernel left without the command (some workgroups may have run
+        // it): the server is gone -- the next eligible run relaunches -- and
+        // the chain state is unusable until replaced
+        e->srv_active = false;
+        e->srv_pending = 0;
+        (void)hipStreamSynchronize(e->stream);   // ended: returns at once
+        (void)hipGetLastError();
+        e->state_lost = true;
+        return fail(PBH_ERR_HIP, "sampling server ended before command %u completed "
+                    "(chain state lost: restore a checkpoint or init the chains)", seq);
       }
-      if (el > std::chrono::seconds(120))
+      if (el > std::chrono::seconds(120)) {
+        e->state_lost = true;
         return fail(PBH_ERR_HIP, "sampling server: command %u not completed in 120 s", seq);
+      }
     }
   }
 }
@@ -856,6 +875,7 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   e->n = n;
   e->off = off;
   e->xo_seeded = false;
+  e->state_lost = false;
   e->has_pred = false;
   e->g = 0;
   e->mom_steps = 0;
@@ -1162,6 +1182,9 @@ static int run_checks(pbh_engine *e, int64_t n_steps) {
   if (!e->has_model || (!e->has_prop && !e->has_gibbs))
     return fail(PBH_ERR_STATE, "model and proposal/gibbs tables must be set");
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
+  if (e->state_lost)
+    return fail(PBH_ERR_STATE, "chain state lost by an incomplete sampling-server command: "
+                "pbh_restore, pbh_set_chains or pbh_init_chains first");
   if (e->has_gibbs != (e->k.scores == PBH_SCORES_GIBBS))
     return fail(PBH_ERR_STATE, "gibbs scores need gibbs tables and vice versa");
   if (n_steps < 0) return fail(PBH_ERR_ARG, "n_steps < 0");
@@ -1272,7 +1295,6 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     if (e->srv_pending) {
       const int rc = srv_wait(e, e->srv_pending, false);
       e->srv_pending = 0;
-      e->srv_last = srv_clk::now();
       if (rc) return rc;
     }
     if (srv_clk::now() - e->srv_last <= std::chrono::milliseconds(e->srv_idle_ms / 2)) {
@@ -1319,7 +1341,6 @@ int pbh_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
         if (e->srv_pending) {   // one command in flight
           const int rc = srv_wait(e, e->srv_pending, false);
           e->srv_pending = 0;
-          e->srv_last = srv_clk::now();
           if (rc) return rc;
         }
         // a server that has ended, or whose idle exit could be near, is
@@ -1507,7 +1528,6 @@ int pbh_sync(pbh_engine *e) {
     if (e->srv_pending) {
       const int rc = srv_wait(e, e->srv_pending, false);
       e->srv_pending = 0;
-      e->srv_last = std::chrono::steady_clock::now();
       return rc;
     }
     return PBH_OK;
@@ -1651,7 +1671,6 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
   if (check_ptr(e, "engine") || check_ptr(x, "x") || check_ptr(lp, "lp"))
     return PBH_ERR_ARG;
   SRV_STOP(e);
-  SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (step < 0) return fail(PBH_ERR_ARG, "step index must be >= 0");
   if (e->rng == PBH_RNG_XOSHIRO && !xo)
@@ -1674,6 +1693,7 @@ int pbh_restore(pbh_engine *e, const double *x, const double *lp, int64_t step,
   e->g = step;
   e->has_pred = has_pred != 0;
   e->gq_valid = false;   // the production Gibbs kernel recomputes g, Q from x
+  e->state_lost = false;
   e->lx_valid = false;   // ... and the ufun logs (pbh_set_chain_logs restores them)
   e->cap = 0;            // a trace / replay rows of the engine are detached
   e->rep_steps = 0;
@@ -1705,6 +1725,7 @@ int pbh_set_chains(pbh_engine *e, const double *x, const double *lp,
   e->gq_valid = false;
   e->lx_valid = false;
   e->cap = 0;            // the trace and the replay rows are detached
+  e->state_lost = false;
   e->rep_steps = 0;
   e->rep_g0 = step;
   return PBH_OK;

@@ -316,6 +316,12 @@ class MainEngine(OracleEngine):
   def legacy_run(self, k, steps_per_launch=0, sync=True):
     assert k >= 1 and steps_per_launch >= 1
     self.run(k, steps_per_launch, sync)
+  def server_info(self):
+    # as if the timed run had been a resident-server command, so that main()
+    # also times the launched form (PBH_SERVER=0) on a fresh engine
+    return {{'active': False, 'commands': 1, 'launches': 1}}
+  def stop_server(self):
+    pass
   def close(self):
     if getattr(self, 'col', None) is not None:
       self.col.close()
@@ -344,6 +350,9 @@ if rank == 0:
   assert line['config']['parallelism'] == 'chain-sharded x{{}}'.format(world)
   assert line['scaling'] == 'weak'
   assert line['replay_chain_steps_per_s'] > 0 and 'REPLAY' in line['replay_config']
+  assert line['launched_chain_steps_per_s'] > 0, line
+  assert line['roofline']['kernel'].endswith('SRV>'), line['roofline']
+  assert not line['launched']['kernel'].endswith('SRV>'), line['launched']
   print('MAIN_OK')
 else:
   assert out == '', out

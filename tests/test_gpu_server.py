@@ -107,6 +107,34 @@ def test_server_leaves_when_idle_and_is_relaunched(monkeypatch):
     assert np.array_equal(tr[k], tr_ref[k]), k
 
 
+def test_server_idle_measured_from_the_submit(monkeypatch):
+  """a sync long after a command must not restart the host's
+  idle clock -- the kernel's workgroups start theirs at the command's
+  completion.  run(sync=False), 0.7 idle later sync, 0.4 idle later run: the
+  kernel has left by then (1.1 idle after the completion), so the run must
+  relaunch it rather than command a server that is gone."""
+  idle = 200
+  eng = _engine(monkeypatch, True, idle_ms=idle)
+  eng.run(1)
+  eng.run(20, sync=False)
+  time.sleep(0.7 * idle / 1e3)
+  eng.sync()
+  time.sleep(0.4 * idle / 1e3)
+  eng.run(20)
+  info = eng.server_info()
+  assert info['launches'] == 2 and info['commands'] == 2, info
+  tr = eng.trace()
+  eng.close()
+  ref = _engine(monkeypatch, False)
+  ref.run(1)
+  ref.run(20)
+  ref.run(20)
+  tr_ref = ref.trace()
+  ref.close()
+  for k in ('v_x', 'v_p', 'u'):
+    assert np.array_equal(tr[k], tr_ref[k]), k
+
+
 def test_server_command_time_and_sync(monkeypatch):
   eng = _engine(monkeypatch, True)
   eng.run(1)
