@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PBH_ABI_VERSION 4
+#define PBH_ABI_VERSION 5
 #define PBH_MAX_DIM 32
 
 #define PBH_OK 0
@@ -276,6 +276,24 @@ int pbh_get_replay(pbh_engine *eng, int64_t first, int64_t n_steps,
  * RNG, after pbh_legacy_seed.  No replay rows are held afterwards.  Replaces
  * the reference's per-step np.random draws + SP.next (sp.py:221-258).      */
 int pbh_legacy_run(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
+/* on != 0: pbh_legacy_run also keeps each step's MH threshold t (the
+ * reference's metropolis_thresh draw, sp_utils.py:30-31, which SP.next
+ * returns as opqrstuv.t, sp.py:249-258) on the device; pbh_get_thresholds
+ * copies steps [first, first + n_steps) of the last pbh_legacy_run as
+ * [n_steps][n_chains].  (The fused kernel stores them as it draws them.)   */
+int pbh_set_record_threshold(pbh_engine *eng, int32_t on);
+int pbh_get_thresholds(pbh_engine *eng, int64_t first, int64_t n_steps, double *out);
+/* The next n_steps draws of every chain's device RandomState (after
+ * pbh_legacy_seed) into out [n_steps][n_chains], the chain's generator
+ * continuing: kind PBH_DRAWS_LINREG draws what the gibbs_linreg example's
+ * cond_reg consumes at global step step0 + t (examples/mcmc/gibbs_linreg.py:
+ * 38-47): standard_gamma(param) when (step0 + t) % 3 == 2, else the legacy
+ * gauss (NumPy's legacy_standard_gamma: Marsaglia-Tsang over the polar gauss
+ * and random_sample, the shape < 1 and shape == 1 branches included);
+ * PBH_DRAWS_GAUSS the legacy gauss every step.                             */
+enum pbh_draws { PBH_DRAWS_GAUSS = 0, PBH_DRAWS_LINREG = 1 };
+int pbh_legacy_draws(pbh_engine *eng, int64_t n_steps, int64_t step0, int32_t kind,
+                     double param, double *out);
 
 /* ---- running (SP.walk / sample_generator: sp.py:281-295, sp_utils.py:8-16) */
 /* Device trace ring for the next runs: every thin-th step is recorded.

@@ -11,7 +11,8 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PBHIP_LIB', os.path.join(_HERE, 'libpbhip.so'))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
+DRAWS_GAUSS, DRAWS_LINREG = 0, 1   # enum pbh_draws
 MAX_DIM = 32
 
 # enums (pbhip.h)
@@ -90,6 +91,11 @@ SIGNATURES = {
     'pbh_legacy_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     'pbh_reserve_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     'pbh_legacy_run': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),
+    'pbh_set_record_threshold': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    'pbh_get_thresholds': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int64, _dp]),
+    'pbh_legacy_draws': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int32, ctypes.c_double, _dp]),
     'pbh_get_replay': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.c_int64, ctypes.c_int32, _dp]),
     'pbh_alloc_trace': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,

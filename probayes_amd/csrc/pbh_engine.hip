@@ -55,6 +55,12 @@ struct pbh_engine {
   bool legacy_k4 = true;       // PBH_LEGACY_K4=0: the round-3 double-buffered state
   bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
   bool legacy_fused = true;    // PBH_LEGACY_FUSED=0: pbh_legacy_run as generation + run
+  bool legacy_wp = true;       // PBH_LEGACY_WP=0: the chain-per-lane generator for MH streams
+  bool mt_odd = false;         // a stream may sit at an odd word (randint drew single words)
+  bool rec_thr = false;        // pbh_set_record_threshold: keep pbh_legacy_run's thresholds
+  double *thr = nullptr;       // [thr_steps][n] thresholds of the last pbh_legacy_run
+  size_t thr_alloc = 0;
+  int64_t thr_steps = 0;
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
   double *mt_gauss = nullptr;
   bool mt_stale = false;       // pbh_restore ran: the streams wait for
@@ -455,6 +461,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *lw = std::getenv("PBH_LEGACY_WIN")) e->legacy_win = std::atoi(lw) != 0;
   if (const char *lk = std::getenv("PBH_LEGACY_K4")) e->legacy_k4 = std::atoi(lk) != 0;
   if (const char *lf = std::getenv("PBH_LEGACY_FUSED")) e->legacy_fused = std::atoi(lf) != 0;
+  if (const char *lp = std::getenv("PBH_LEGACY_WP")) e->legacy_wp = std::atoi(lp) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
   // A/B switch for the markers' fences; default 0 = hipEventDefault)
   unsigned ev_flags = 0;
@@ -487,6 +494,7 @@ int pbh_destroy(pbh_engine *e) {
   if (e->comm) ncclCommDestroy(e->comm);
   dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
   dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq); dfree(e->lx);
+  dfree(e->thr);
   dfree(e->mt_key); dfree(e->mt_pos); dfree(e->mt_has); dfree(e->mt_order);
   dfree(e->mt_gauss);
   free_trace(e);
@@ -857,11 +865,9 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
     if (!rc) rc = dalloc(e->ess, (size_t)d * n);
     if (rc) return rc;
   }
-  {
-    std::vector<double> nan((size_t)d * n, std::nan(""));
-    HIP_TRY(hipMemcpy(e->ess, nan.data(), nan.size() * sizeof(double),
-                      hipMemcpyHostToDevice));
-  }
+  // no ESS computed yet: every byte 0xFF is a NaN (all-ones exponent and
+  // mantissa), set on the device instead of copying a host array of NaNs
+  HIP_TRY(hipMemset(e->ess, 0xFF, (size_t)d * n * sizeof(double)));
   e->gq_valid = false;
   e->lx_valid = false;
   std::vector<double> xt((size_t)n * d);
@@ -964,6 +970,7 @@ int pbh_legacy_seed(pbh_engine *e, const uint32_t *seeds) {
                : (e->legacy_k4 && e->legacy_win && mt_words(2) * 4 * n < (int64_t(1) << 32)) ? 2
                                                                                           : 1;
   e->mt_stale = false;
+  e->mt_odd = false;
   int rc = dalloc(e->mt_key, (size_t)mt_words(e->mt_mode) * n);
   if (!rc) rc = dalloc(e->mt_pos, n);
   if (!rc) rc = dalloc(e->mt_has, n);
@@ -1042,6 +1049,8 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   a.win = e->legacy_win ? 1 : 0;
   a.vmode = e->k.vmode;
   a.vdelta = e->k.pdel;
+  a.wp = (e->legacy_wp && !e->mt_odd) ? 1 : 0;
+  if (a.vardelta) e->mt_odd = true;   // randint may leave odd positions
   if (!e->lgtab) {
     std::vector<double> lt(pbh::kLegLogDoubles);
     pbh::legacy_log_table(lt.data());
@@ -1465,14 +1474,29 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   for (int j = 0; j < (int)e->draw_order.size(); ++j) ident = ident && e->draw_order[j] == j;
   const bool fused = e->legacy_fused && ident &&
                      pbh::launch_legacy_mh(la, k, e->stream, true) == hipSuccess;
+  // the thresholds (pbh_set_record_threshold): MH only (Gibbs draws none)
+  const bool keep_thr = e->rec_thr && !e->has_gibbs;
+  e->thr_steps = 0;
+  if (keep_thr && e->thr_alloc < (size_t)n_steps * e->n) {
+    if (const int rc = dalloc(e->thr, (size_t)n_steps * e->n)) {
+      e->thr_alloc = 0;
+      return rc;
+    }
+    e->thr_alloc = (size_t)n_steps * e->n;
+  }
   if (!fused) {
     for (int64_t done = 0; done < n_steps;) {
       const int64_t m = std::min(spl, n_steps - done);
       int rc = pbh_legacy_replay(e, m);
+      if (!rc && keep_thr)   // the stream's threshold row, [m][n]
+        HIP_TRY(hipMemcpy2DAsync(e->thr + (size_t)done * e->n, e->n * sizeof(double),
+                                 e->rep + (size_t)e->d * e->n, (size_t)R * e->n * sizeof(double),
+                                 e->n * sizeof(double), m, hipMemcpyDeviceToDevice, e->stream));
       if (!rc) rc = pbh_run(e, m, 0);
       if (rc) return rc;
       done += m;
     }
+    e->thr_steps = keep_thr ? n_steps : 0;
     return PBH_OK;
   }
   e->srv_timed = false;
@@ -1498,6 +1522,7 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
     k.lx_init = 1;
     la.n_steps = m;
     la.step0 = e->g;
+    la.thr = keep_thr ? e->thr + (size_t)done * e->n : nullptr;
     const hipError_t err = pbh::launch_legacy_mh(la, k, e->stream, false);
     if (err != hipSuccess) {
       lev = {};
@@ -1512,6 +1537,7 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   if (e->event_markers) HIP_TRY(hipEventRecord(e->ev1, e->stream));
   e->gq_valid = false;
   e->lx_valid = false;
+  e->thr_steps = keep_thr ? n_steps : 0;
   // the stream rows are not written: none are held from here on
   e->k.R = R;
   e->rep_steps = 0;
@@ -1519,6 +1545,58 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   e->mom_steps += n_steps;
   e->timed = true;
   e->last_launches = launches;
+  return PBH_OK;
+}
+
+int pbh_set_record_threshold(pbh_engine *e, int32_t on) {
+  if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  e->rec_thr = on != 0;
+  return PBH_OK;
+}
+
+int pbh_get_thresholds(pbh_engine *e, int64_t first, int64_t n_steps, double *out) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  if (first < 0 || n_steps < 0 || first + n_steps > e->thr_steps)
+    return fail(PBH_ERR_ARG, "thresholds [%lld, %lld) not held (%lld kept by the last "
+                "pbh_legacy_run; pbh_set_record_threshold first)", (long long)first,
+                (long long)(first + n_steps), (long long)e->thr_steps);
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(out, e->thr + (size_t)first * e->n, (size_t)n_steps * e->n * sizeof(double),
+                    hipMemcpyDeviceToHost));
+  return PBH_OK;
+}
+
+int pbh_legacy_draws(pbh_engine *e, int64_t n_steps, int64_t step0, int32_t kind,
+                     double param, double *out) {
+  if (check_ptr(e, "engine") || check_ptr(out, "out")) return PBH_ERR_ARG;
+  SRV_STOP(e);
+  if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first");
+  if (e->mt_stale)
+    return fail(PBH_ERR_STATE, "pbh_restore ran after pbh_legacy_seed: set the "
+                "checkpoint's legacy state (pbh_set_legacy_state) first");
+  if (e->mt_mode != 2) return fail(PBH_ERR_UNSUPPORTED, "pbh_legacy_draws needs the Mt4 state");
+  if (kind != PBH_DRAWS_GAUSS && kind != PBH_DRAWS_LINREG)
+    return fail(PBH_ERR_ARG, "bad draws kind %d", kind);
+  if (n_steps < 0 || step0 < 0) return fail(PBH_ERR_ARG, "n_steps, step0 must be >= 0");
+  if (!(param >= 0.0)) return fail(PBH_ERR_ARG, "gamma shape must be >= 0");
+  if (n_steps == 0) return PBH_OK;
+  const int64_t n = e->n;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  double *dout = nullptr;
+  if (const int rc = dalloc(dout, (size_t)n_steps * n)) return rc;
+  pbh::LegacyArgs a{};
+  a.key = e->mt_key; a.pos = e->mt_pos; a.gauss = e->mt_gauss; a.has_gauss = e->mt_has;
+  a.out = dout; a.n = n; a.n_steps = n_steps; a.step0 = step0; a.d = 1; a.R = 1;
+  a.db = e->mt_mode;
+  hipError_t err = pbh::launch_legacy_draws(a, kind, param, e->stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+  if (err == hipSuccess)
+    err = hipMemcpy(out, dout, (size_t)n_steps * n * sizeof(double), hipMemcpyDeviceToHost);
+  dfree(dout);
+  if (err != hipSuccess) return fail(PBH_ERR_HIP, "pbh_legacy_draws: %s", hipGetErrorString(err));
   return PBH_OK;
 }
 
@@ -1803,6 +1881,8 @@ int pbh_set_legacy_state(pbh_engine *e, const uint32_t *key, const int32_t *pos,
   HIP_TRY(hipMemcpy(e->mt_has, has, n * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->mt_gauss, gauss, n * sizeof(double), hipMemcpyHostToDevice));
   e->mt_stale = false;
+  e->mt_odd = false;
+  for (int64_t c = 0; c < n && !e->mt_odd; ++c) e->mt_odd = (pos[c] & 1) != 0;
   return PBH_OK;
 }
 

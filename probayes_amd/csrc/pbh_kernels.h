@@ -235,7 +235,15 @@ struct LegacyArgs {
   uint64_t vmode;
   const double *vdelta;
   const double *lgtab;  // legacy_log_table (Mt4's polar log)
+  int32_t wp;           // with db == 2: the word-parallel generator for MH
+                        // streams of doubles (every position even)
+  double *thr;          // the fused kernel: each step's threshold [n_steps][n]
+                        // (nullptr: not kept)
 };
+// pbh_legacy_draws: per chain, n_steps draws of kind (pbh_draws) into a.out
+// [n_steps][n] (Mt4 state)
+hipError_t launch_legacy_draws(const LegacyArgs &a, int32_t kind, double param,
+                               hipStream_t s);
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
                               int64_t n, int32_t db, hipStream_t s);

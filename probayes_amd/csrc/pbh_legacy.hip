@@ -23,13 +23,12 @@
 #include "pbh_kernels.h"
 #include "pbh_kernels_impl.h"   // mh_body: the fused REPLAY kernel
 #include "pbhip.h"
+#include "pbh_mt.h"
 
 namespace pbh {
 namespace {
 
-constexpr int kN = 624, kM = 397;
 constexpr int kBlockLegacy = 256;   // threads per workgroup of the generators
-constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
 
 __global__ __launch_bounds__(256) void mt_seed_kernel(uint32_t *key, int32_t *pos,
                                                       double *gauss, int32_t *has_gauss,
@@ -135,12 +134,7 @@ struct Mt {
 // q + 1, words 4q + 397 .. + 400 (quads q + 99, q + 100, at offset 1) or
 // dst words 4q - 227 .. - 224 (quads q - 57, q - 56, at offset 1).
 // Per-lane state word: pos | buf << 16 | pending << 17.
-constexpr int kQ = kN / 4;   // 156 quads per block
 
-__device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b) {
-  const uint32_t y = (a & kUpper) | (b & kLower);
-  return (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-}
 
 struct Mt2 {
   static constexpr bool kLockstep = true;
@@ -270,7 +264,6 @@ struct Mt2 {
 // 1 or an earlier batch), so ~30 loads are in flight instead of two.
 // a quad as a plain vector (SROA splits arrays of it into registers; arrays
 // of HIP's uint4 struct stayed in scratch)
-typedef uint32_t w4 __attribute__((ext_vector_type(4)));
 
 // a block -> the next block: ld(0, i) / ld(1, i) read quad i of the source /
 // destination block, st(i, v) writes quad i of the destination
@@ -628,10 +621,6 @@ struct Mt3 {
 // whatever the other lanes' positions.
 // Packed state: pos | cb << 16 | ready << 18 (cb = the current block's buffer).
 // ---------------------------------------------------------------------------
-constexpr int kK4 = 4, kCh = 20;   // buffers; 8-quad chunks per (padded) block
-__device__ __forceinline__ w4 &k4q(w4 *key, int64_t n, int64_t c, int b, int i) {
-  return key[((int64_t)(b * kCh + (i >> 3)) * n + c) * 8 + (i & 7)];
-}
 // The twist through a raw buffer resource over the whole state (the engine
 // takes this layout only while it spans < 2^32 bytes): each lane's source and
 // destination buffers are one per-lane byte offset each, and every quad's
@@ -671,18 +660,6 @@ __device__ __forceinline__ void mt4_load(w4 *key, int64_t n, int64_t c, int b, i
     const v4u t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, u * 16, 0);
     v[u] = w4{t.x, t.y, t.z, t.w};
   }
-}
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  y ^= y >> 18;
-  return y;
-}
-// random_sample of two raw words (tempered here)
-__device__ __forceinline__ double mt_dbl(uint32_t wa, uint32_t wb) {
-  const int32_t a = (int32_t)(mt_temper(wa) >> 5), b = (int32_t)(mt_temper(wb) >> 6);
-  return (a * 67108864.0 + b) / 9007199254740992.0;
 }
 // DBL: the ring holds each quad as the two random_sample doubles of its
 // word pairs (every draw of the Normal / Raw / Gibbs streams is a double at
@@ -1075,35 +1052,6 @@ __global__ __launch_bounds__(256) void mt_seed_db_kernel(uint32_t *key, int32_t 
 constexpr int kModeAny = -1, kModeGibbs = 0, kModeVardelta = 1, kModeNormal = 2,
               kModeRaw = 3;
 
-// log(x) of the polar method's r2 in (0, 1) (a normal double) for Mt4
-// (Tang's table method): x = m 2^e, m in [1/2, 1), c = m rounded to 1/256,
-// r = (m - c) / c (|r| <= 2^-8; m - c exact), log x = (e ln2_hi + T_hi) +
-// (r + (r^2 q(r) + (e ln2_lo + T_lo))) with ln c = T_hi + T_lo, T_hi and
-// ln2_hi multiples of 2^-32 so that their sum is exact, q the log1p series
-// to r^8 (truncation < 2^-70 relative).  About 20 VALU and two LDS reads
-// against ~75 VALU for OCML's log; within ~0.5 ulp, so the normals stay
-// within the last ulp of NumPy's (tests/test_gpu_legacy.py).
-__device__ __forceinline__ double log_leg(double x, const double *tab) {
-  const double m = __builtin_amdgcn_frexp_mant(x);
-  const int e = __builtin_amdgcn_frexp_exp(x);
-  const uint32_t ch = ((uint32_t)(__builtin_bit_cast(uint64_t, m) >> 32) + 0x1000u) & 0xFFFFE000u;
-  const uint32_t off = (ch >> 9) & 0xFFFu;   // 16 j
-  const char *tb = reinterpret_cast<const char *>(tab);
-  const double2 t = *reinterpret_cast<const double2 *>(tb + off);
-  const double ic = *reinterpret_cast<const double *>(tb + kLegLogInv * 8 + (off >> 1));
-  const double r = (m - __builtin_bit_cast(double, (uint64_t)ch << 32)) * ic;
-  double q = __builtin_fma(r, -1.0 / 8.0, 1.0 / 7.0);
-  q = __builtin_fma(q, r, -1.0 / 6.0);
-  q = __builtin_fma(q, r, 1.0 / 5.0);
-  q = __builtin_fma(q, r, -1.0 / 4.0);
-  q = __builtin_fma(q, r, 1.0 / 3.0);
-  q = __builtin_fma(q, r, -0.5);
-  const double de = (double)e;
-  const double lo = __builtin_fma(de, 1.90821492927058770002e-10, t.y);
-  const double shi = __builtin_fma(de, 6.93147180369123816490e-01, t.x);   // exact
-  const double p = __builtin_fma(r * r, q, lo);
-  return shi + (r + p);
-}
 
 // The polar method's attempts of one step (legacy_gauss's draws): lanes run
 // the ATTEMPTS in lockstep (one per iteration until each holds its `need`
@@ -1423,6 +1371,77 @@ hipError_t launch_win(const LegacyArgs &a, hipStream_t s) {
   return launch_win_mode<H, kModeRaw>(a, s);
 }
 
+// legacy_standard_exponential (legacy-distributions.c): -log(1 - random_sample)
+template <class M>
+__device__ __forceinline__ double legacy_exponential(M &m) {
+  return -log(1.0 - m.next_double());
+}
+
+// NumPy's legacy_standard_gamma (random/src/legacy/legacy-distributions.c,
+// the numpy 2.2.6 pinned in SURVEY.md §8c): Marsaglia-Tsang for shape > 1
+// over the polar legacy gauss (its cached deviate included) and
+// random_sample -- the squeeze 1 - 0.0331 x^4, then the log test -- and
+// Johnk-style rejection for shape < 1; shape 1 is the exponential.  The
+// operations and their order are NumPy's (-ffp-contract=off: no FMA).
+template <class M>
+__device__ double legacy_gamma(M &m, double &gauss, int &has, double shape) {
+  if (shape == 1.0) return legacy_exponential(m);
+  if (shape == 0.0) return 0.0;
+  if (shape < 1.0) {
+    for (;;) {
+      const double U = m.next_double();
+      const double V = legacy_exponential(m);
+      if (U <= 1.0 - shape) {
+        const double X = pow(U, 1. / shape);
+        if (X <= V) return X;
+      } else {
+        const double Y = -log((1 - U) / shape);
+        const double X = pow(1.0 - shape + shape * Y, 1. / shape);
+        if (X <= (V + Y)) return X;
+      }
+    }
+  }
+  const double b = shape - 1. / 3.;
+  const double c = 1. / sqrt(9 * b);
+  for (;;) {
+    double X, V;
+    do {
+      X = legacy_gauss(m, gauss, has);
+      V = 1.0 + c * X;
+    } while (V <= 0.0);
+    V = V * V * V;
+    const double U = m.next_double();
+    if (U < 1.0 - 0.0331 * (X * X) * (X * X)) return (b * V);
+    if (log(U) < 0.5 * X * X + b * (1. - V + log(V))) return (b * V);
+  }
+}
+
+// pbh_legacy_draws: one chain per lane on Mt4's state through its window,
+// the draws of each step in the reference's order, out [n_steps][n]
+template <int H>
+__global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void legacy_draws_kernel(LegacyArgs a, int32_t kind, double param) {
+  extern __shared__ w4 s_lw[];
+  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
+  if (c >= a.n) return;
+  Mt4<H, true> m;
+  m.key = reinterpret_cast<w4 *>(a.key);
+  m.n = a.n;
+  m.c = c;
+  m.init(a.pos[c], s_lw + threadIdx.x);
+  double gauss = a.gauss[c];
+  int has = a.has_gauss[c];
+  __builtin_amdgcn_s_waitcnt(0);
+  for (int64_t t = 0; t < a.n_steps; ++t) {
+    m.maintain();   // wave-uniform: every active lane is here
+    const bool gam = kind == PBH_DRAWS_LINREG && (a.step0 + t) % 3 == 2;
+    a.out[t * a.n + c] = gam ? legacy_gamma(m, gauss, has, param) : legacy_gauss(m, gauss, has);
+  }
+  a.pos[c] = m.packed();
+  a.gauss[c] = gauss;
+  a.has_gauss[c] = has;
+}
+
 // ---------------------------------------------------------------------------
 // Fused REPLAY (legacy_mh_kernel): the generator and the REPLAY chain-step in
 // one kernel.  The two-kernel form writes the [T][R][N] stream (1.44 GB per
@@ -1447,6 +1466,8 @@ struct LegacyDraws {
   const double *s_lg;
   double gauss;
   int has;
+  double *thr_out;   // [n_steps][n] thresholds (pbh_set_record_threshold) or nullptr
+  int64_t n;
 
   // every load before the step loop completes here, once (see legacy_gen_body)
   __device__ __forceinline__ void begin() { __builtin_amdgcn_s_waitcnt(0); }
@@ -1479,7 +1500,7 @@ struct LegacyDraws {
   }
 
   template <int D>
-  __device__ __forceinline__ void draws(const KArgs &, int, int64_t, double (&r)[D],
+  __device__ __forceinline__ void draws(const KArgs &, int s, int64_t cc, double (&r)[D],
                                         double &thr) {
     m.maintain();   // wave-uniform: every active lane is here
     if constexpr (NORMAL) {
@@ -1493,6 +1514,7 @@ struct LegacyDraws {
       for (int k = 0; k < D; ++k) r[k] = m.next_double();
     }
     thr = m.next_double();   // the MH threshold
+    if (thr_out) thr_out[(int64_t)s * n + cc] = thr;
   }
 };
 
@@ -1513,7 +1535,7 @@ void legacy_mh_kernel(LegacyArgs la, KArgs a) {
   m.c = c;
   m.init(la.pos[c], s_lw + threadIdx.x);
   LegacyDraws<M, NORMAL> src{m, reinterpret_cast<double2 *>(s_lw + 2 * H * kBlockLegacy), s_lg,
-                             la.gauss[c], la.has_gauss[c]};
+                             la.gauss[c], la.has_gauss[c], la.thr, la.n};
   mh_body<D, PBH_RNG_REPLAY, TGT, PROP>(a, src, nullptr, false);
   la.pos[c] = m.packed();
   la.gauss[c] = src.gauss;
@@ -1550,6 +1572,8 @@ hipError_t launch_legacy_mh_d(const LegacyArgs &la, const KArgs &a, hipStream_t 
   return launch_legacy_mh_t<D, 16, false, 0, 0>(la, a, s);
 }
 
+
+
 }  // namespace
 
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
@@ -1568,7 +1592,25 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
   return hipGetLastError();
 }
 
+// the word-parallel generator (pbh_legacy_wp.hip)
+hipError_t launch_legacy_wp(const LegacyArgs &a, hipStream_t s);
+
+hipError_t launch_legacy_draws(const LegacyArgs &a, int32_t kind, double param,
+                               hipStream_t s) {
+  if (a.db != 2) return hipErrorNotSupported;   // the Mt4 state
+  constexpr int H = 16;
+  const size_t lds = (size_t)(2 * H) * kBlockLegacy * sizeof(uint4);
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void *>(&legacy_draws_kernel<H>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  const dim3 grid((unsigned)((a.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+  hipLaunchKernelGGL(legacy_draws_kernel<H>, grid, block, lds, s, a, kind, param);
+  return hipGetLastError();
+}
+
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s) {
+  // the word-parallel generator: Mt4's state, MH streams of doubles
+  if (a.db == 2 && a.wp && !a.gibbs && !a.vardelta) return launch_legacy_wp(a, s);
   if (a.db == 2) {   // Mt4: four chunked blocks through the window
     if (!a.normal || a.d <= 12) return launch_k4<16>(a, s);
     return launch_k4<8>(a, s);

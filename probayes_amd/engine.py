@@ -303,6 +303,30 @@ class Engine:
     if sync:
       self.sync()
 
+  def set_record_threshold(self, on=True):
+    """Keep each step's MH threshold t of the next legacy_run calls on the
+    device (get_thresholds)."""
+    _lib.call('pbh_set_record_threshold', self._h, 1 if on else 0)
+
+  def get_thresholds(self, first, n_steps):
+    """Thresholds of steps [first, first + n_steps) of the last legacy_run
+    (set_record_threshold first): [n_steps, N]."""
+    out = np.empty((int(n_steps), self.n), np.float64)
+    _lib.call('pbh_get_thresholds', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(n_steps)), _dp(out))
+    return out
+
+  def legacy_draws(self, n_steps, step0=0, kind='linreg', param=1.0):
+    """The next n_steps draws of every chain's device RandomState, [n_steps,
+    N]: kind 'linreg' -- standard_gamma(param) on steps (step0 + t) % 3 == 2,
+    the legacy gauss otherwise (gibbs_linreg's cond_reg order); 'gauss' --
+    the legacy gauss every step."""
+    k = {'gauss': _lib.DRAWS_GAUSS, 'linreg': _lib.DRAWS_LINREG}[kind]
+    out = np.empty((int(n_steps), self.n), np.float64)
+    _lib.call('pbh_legacy_draws', self._h, _c.c_int64(int(n_steps)),
+              _c.c_int64(int(step0)), k, _c.c_double(float(param)), _dp(out))
+    return out
+
   def sync(self):
     rc = self._fn_sync(self._h)
     if rc:

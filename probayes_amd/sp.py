@@ -583,7 +583,7 @@ class SP:
     if self._counter is None:
       self._counter = _WeakCounter()
     if self._last is None:
-      self._last = weakref.WeakKeyDictionary()
+      self._last = _LastStates()
     if sampler_id is None:
       return None
     sampler = self.get_sampler(sampler_id)
@@ -624,7 +624,7 @@ class SP:
       self.reset()
     step = sampler._next_step()
     self._counter[sampler] += sampler.thin
-    self._last[sampler] = OPQR(None, step.v, None, None)
+    self._last[sampler] = step   # OPQR(None, step.v, None, None) when read
     return step
 
   # ---- sampling (sp.py:261-295) ---------------------------------------------
@@ -683,6 +683,29 @@ class SP:
     return summary
 
 
+class _LastStates(weakref.WeakKeyDictionary):
+  """SP's last states (sp.py:254-255: the last accepted opqr per sampler),
+  kept as the last Step handed out and made the reference's
+  OPQR(None, v, None, None) when read: handing out a step never copies a
+  device-resident trace to the host."""
+
+  def __getitem__(self, key):
+    v = super().__getitem__(key)
+    if isinstance(v, Step):
+      v = OPQR(None, v.v, None, None)
+      super().__setitem__(key, v)
+    return v
+
+  def get(self, key, default=None):
+    return self[key] if key in self else default
+
+  def values(self):
+    return [self[k] for k in list(self.keys())]
+
+  def items(self):
+    return [(k, self[k]) for k in list(self.keys())]
+
+
 class _WeakCounter(weakref.WeakKeyDictionary):
   """SP's step counters (sp.py:113-128: a collections.Counter keyed by
   sampler) without keeping the samplers alive: a sampler dropped by the
@@ -698,19 +721,84 @@ OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',
 OPQR = collections.namedtuple('opqr', ['o', 'p', 'q', 'r'])
 
 
+class _DeviceTrace:
+  """A block's trace arrays (v_x [N, T, d], v_p [N, T], u [N, T]; debug
+  p_x, p_p, s) left in the engine's device trace until first read: a
+  sampler's steps are handed out without copying T x N x (8d + 9) bytes to
+  the host, and a caller who reduces on the device or reads a few steps never
+  pays for the rest.  The sampler copies it (materialize) before anything
+  reuses the engine's trace."""
+
+  __slots__ = ('_eng', '_keys', '_data')
+
+  def __init__(self, eng, debug):
+    self._eng = eng
+    self._keys = ('v_x', 'v_p', 'u') + (('p_x', 'p_p', 's') if debug else ())
+    self._data = None
+
+  def materialize(self):
+    if self._data is None:
+      self._data = self._eng.trace()
+      self._eng = None
+    return self._data
+
+  def __getitem__(self, key):
+    return self.materialize()[key]
+
+  def get(self, key, default=None):
+    return self[key] if key in self._keys else default
+
+  def __contains__(self, key):
+    return key in self._keys
+
+  def keys(self):
+    return self._keys
+
+
+class _LazyPrev:
+  """A block's last record (x [N, d], lp [N]) as the next block's
+  predecessor state, read when that block is computed -- after _settle has
+  copied the block to the host."""
+
+  __slots__ = ('block',)
+
+  def __init__(self, block):
+    self.block = block
+
+  def __iter__(self):
+    tr = self.block.tr
+    return iter((np.array(tr['v_x'][:, -1, :]), np.array(tr['v_p'][:, -1])))
+
+
 class _Block:
   """Records [0, T) of one engine run of a sampler: trace arrays tr (v_x
-  [N, T, d], v_p [N, T], u [N, T]; debug p_x, p_p, s), thresholds [N, T] or
-  None, the state before record 0 (prev_x [N, d], prev_p [N]), whether
-  record 0 is step 1 of a sampler epoch (first: no predecessor), the global
-  step of its first step (g0), and what a rewind into it needs (rewind)."""
+  [N, T, d], v_p [N, T], u [N, T]; debug p_x, p_p, s; a dict or a
+  _DeviceTrace), thresholds [N, T] or None (or a function that copies them
+  from the engine's replay rows), the state before record 0 (prev_x [N, d],
+  prev_p [N]), whether record 0 is step 1 of a sampler epoch (first: no
+  predecessor), the global step of its first step (g0), and what a rewind
+  into it needs (rewind)."""
 
-  __slots__ = ('tr', 'thr', 'prev_x', 'prev_p', 'first', 'g0', 'T', 'rewind')
+  __slots__ = ('tr', '_thr', '_thr_fn', 'prev_x', 'prev_p', 'first', 'g0', 'T',
+               'rewind')
 
-  def __init__(self, tr, thr, prev_x, prev_p, first, g0, rewind):
-    self.tr, self.thr, self.prev_x, self.prev_p = tr, thr, prev_x, prev_p
+  def __init__(self, tr, thr, prev_x, prev_p, first, g0, rewind, T=None):
+    self.tr, self.prev_x, self.prev_p = tr, prev_x, prev_p
+    self._thr, self._thr_fn = (None, thr) if callable(thr) else (thr, None)
     self.first, self.g0, self.rewind = first, g0, rewind
-    self.T = tr['v_x'].shape[1]
+    self.T = tr['v_x'].shape[1] if T is None else T
+
+  @property
+  def thr(self):
+    if self._thr_fn is not None:
+      self._thr, self._thr_fn = self._thr_fn(), None
+    return self._thr
+
+  def materialize(self):
+    """Copies whatever still sits in the engine (before it is reused)."""
+    if isinstance(self.tr, _DeviceTrace):
+      self.tr.materialize()
+    _ = self.thr
 
 
 class Step:
@@ -824,7 +912,7 @@ class Sampler:
     self.spec = None
     self._eng = None        # the engine (MH / CondCov Gibbs)
     self._lx = None         # linreg: the chains' state [N, 3] (host)
-    self._rs = None         # linreg legacy streams: RandomState per chain
+    self._rs = None         # linreg legacy streams: an Engine of device RandomStates
     self._g = 0             # global step of the next step to compute
     self._cur = None        # block being handed out and its next record
     self._j = 0
@@ -838,6 +926,7 @@ class Sampler:
     # per step instead of a redraw of the whole remaining stop)
     self._ahead = self.chunk
     self.n_computed = 0     # chain-steps' worth of steps run (diagnostic)
+    self._prev = None       # the state before the next block, when known on the host
 
   def __repr__(self):
     return '<probayes_amd Sampler {} stop={}>'.format(self.sid, self.stop)
@@ -901,6 +990,7 @@ class Sampler:
   def _start_epoch(self):
     """Chains back at init, step 1 next (auto-accept); a Gibbs cycle starts
     at its RF's phase; every generator continues."""
+    self._settle()
     gibbs = self._is_gibbs()
     phase = getattr(self._cycle_rf(), '_pbh_cond_step', 0) if gibbs else 0
     g = self._g
@@ -910,8 +1000,7 @@ class Sampler:
     if self.spec.get('kind') == 'linreg':
       self._lx = init
       if self.rng == 'legacy' and self.seeds is not None and self._rs is None:
-        self._rs = [np.random.RandomState(int(s)) for s in
-                    np.asarray(self.seeds).reshape(-1)]
+        self._rs = self._linreg_streams()
     elif self._eng is None:
       eng = Engine(self.spec, device=self.device)
       self._eng = eng
@@ -921,18 +1010,31 @@ class Sampler:
       if self.rng == 'legacy':
         eng.set_rng('replay')
         if self.seeds is not None:
-          # RandomState(seeds[c]) per chain, generated on the device
+          # RandomState(seeds[c]) per chain, generated on the device; the MH
+          # thresholds kept for the steps' t
           eng.seed_legacy(np.asarray(self.seeds))
+          if self.spec['proposal']['kind'] != 'gibbs':
+            eng.set_record_threshold(True)
       else:
         eng.set_rng(self.rng, self.seed)
     else:
       self._eng.set_chains(init, np.zeros(self.n), g, False)
     self._g = g
     self._epoch_first = True
+    # the state before the epoch's first step: init, lp 0 (as init_chains /
+    # set_chains leave it)
+    self._prev = (init, np.zeros(self.n))
 
   def close(self):
     """Frees the engine (also done when the sampler is collected)."""
+    if self._rs is not None:   # the linreg chains' device RandomStates
+      self._rs.close()
+      self._rs = None
     if self._eng is not None:
+      try:
+        self._settle()   # steps handed out keep their data
+      except Exception:   # a failed engine: nothing to copy
+        pass
       self._eng.close()
       self._eng = None
 
@@ -971,8 +1073,15 @@ class Sampler:
       states.append(_GlobalStream.state())
     return np.concatenate(out, axis=0), states
 
+  def _settle(self):
+    """Copies the current block's data still held by the engine (its trace,
+    its replay rows) before the engine runs, rewinds or reseeds again."""
+    if self._cur is not None:
+      self._cur.materialize()
+
   def _compute(self):
     """Runs the next block from the current chain state."""
+    self._settle()
     k = self._block_steps()
     first = self._epoch_first
     self._epoch_first = False
@@ -987,11 +1096,19 @@ class Sampler:
     if self._global_stream():
       self._ahead = min(2 * self._ahead, 1 << 30)
     # Steps keep their own block; the sampler keeps only the current one
-    self._cur, self._j = _Block(tr, thr, prev_x, prev_p, first, g0, rewind), 0
+    self._cur, self._j = _Block(tr, thr, prev_x, prev_p, first, g0, rewind,
+                                T=k // self.thin), 0
+    # the next block's predecessor state: this block's last record (read
+    # from the host copy _settle makes before that block runs)
+    cur = self._cur
+    self._prev = None if self._is_gibbs() else _LazyPrev(cur)   # (MH: lp = v.prob)
 
   def _compute_engine(self, k, rewind):
     eng = self._eng
-    prev_x, prev_p = eng.state()
+    if self._prev is not None:   # known on the host: no device copy
+      prev_x, prev_p = tuple(self._prev)
+    else:
+      prev_x, prev_p = eng.state()
     thr = None
     if self.rng == 'legacy':
       if self.seeds is None:
@@ -999,17 +1116,23 @@ class Sampler:
         eng.upload_replay(streams)
         thr = streams[:, -1, :] if self.spec['proposal']['kind'] != 'gibbs' else None
       else:
-        eng.legacy_replay(k)
+        # the device RandomStates drawn inside the REPLAY steps (the fused
+        # kernel, pbh_legacy_run); the thresholds stay on the device until a
+        # step's t or the summary reads them
         self._drawn.append((self._g, k))   # steps drawn since seeding
-        thr = eng.get_replay(0, k, eng.stream_width() - 1) \
-            if self.spec['proposal']['kind'] != 'gibbs' else None
-      if thr is not None:
+        eng.alloc_trace(k // self.thin, self.thin, debug=self.debug)
+        eng.legacy_run(k, steps_per_launch=self.spl)
+        if self.spec['proposal']['kind'] != 'gibbs':
+          thin = self.thin
+          thr = lambda: eng.get_thresholds(0, k).T[:, thin - 1::thin]
+        return _DeviceTrace(eng, self.debug), thr, prev_x, prev_p
+      if isinstance(thr, np.ndarray):
         thr = thr.T[:, self.thin - 1::self.thin]
     elif self.rng == 'xoshiro':
       rewind['ck'] = eng.checkpoint()     # the generators at block start
     eng.alloc_trace(k // self.thin, self.thin, debug=self.debug)
     eng.run(k, steps_per_launch=self.spl)
-    return eng.trace(), thr, prev_x, prev_p
+    return _DeviceTrace(eng, self.debug), thr, prev_x, prev_p
 
   def _compute_linreg(self, k, rewind):
     sp = self.spec
@@ -1034,14 +1157,25 @@ class Sampler:
 
   def _linreg_draws(self, g, k, keep=True):
     """k steps from the seeded per-chain RandomStates (linreg's legacy
-    order: standard_gamma on y_sigma steps, gauss otherwise)."""
+    order: standard_gamma on y_sigma steps, gauss otherwise), drawn on the
+    device (pbh_legacy_draws: one NumPy RandomState per chain, NumPy's
+    legacy_standard_gamma): [k, N]."""
     alpha = self.spec['hyper'][4] + 0.5 * len(self.spec['x_obs'])
-    rand = np.empty((k, len(self._rs)))
-    for c, r in enumerate(self._rs):
-      for t in range(k):
-        rand[t, c] = r.standard_gamma(alpha) if (g + t) % 3 == 2 \
-            else r.standard_normal()
-    return rand
+    return self._rs.legacy_draws(k, g, 'linreg', alpha)
+
+  def _linreg_streams(self):
+    """The seeded linreg chains' RandomStates on the device: an engine
+    that holds only the legacy generators (pbh_legacy_seed)."""
+    from probayes_amd.spec import make_spec
+    eng = Engine(make_spec(1, target={'kind': 'diag_gauss', 'mu': np.zeros(1),
+                                      'sigma': np.ones(1)},
+                           proposal={'kind': 'gauss', 'loc': 0., 'scale': 1.},
+                           scores='hastings', pscale='log',
+                           tran={'kind': 'const', 'value': 1.0, 'sym': True}),
+                 device=self.device)
+    eng.init_chains(np.zeros((self.n, 1)))
+    eng.seed_legacy(np.asarray(self.seeds))
+    return eng
 
   def _reseed_streams(self, keep):
     """Rewinds the seeded legacy streams to the draws of the first `keep`
@@ -1051,8 +1185,7 @@ class Sampler:
     log, self._drawn = self._drawn, []
     linreg_ = self.spec.get('kind') == 'linreg'
     if linreg_:
-      self._rs = [np.random.RandomState(int(s)) for s in
-                  np.asarray(self.seeds).reshape(-1)]
+      self._rs.seed_legacy(np.asarray(self.seeds))
     else:
       eng = self._eng
       eng.seed_legacy(np.asarray(self.seeds))
@@ -1104,6 +1237,7 @@ class Sampler:
   def _rewind_to_handed(self):
     """Puts the chains (and their generators) where the last step handed
     out left them: the engine may have run ahead of it."""
+    self._settle()
     cur = self._cur
     if cur is None or self._j >= cur.T:
       return   # nothing ahead
@@ -1135,6 +1269,7 @@ class Sampler:
     self._g = g
     self._epoch_first = j < 0 and cur.first
     self._cur, self._j = None, 0
+    self._prev = None   # the engine holds the rewound state
 
   def _reset(self, reset_last):
     """SP.reset: reset_last restarts the chains at init at the next step;

@@ -111,6 +111,13 @@ def test_batched_sampler_reproduces_all_reference_chains(name):
     got = np.asarray(summary.v[k]).T            # [N, T]
     assert _golden_rtol(got, g['v_x'][:, :, i]) <= 1e-12
   assert summary.u.count(True) == int(g['u'].sum())
+  if sampler.spec['proposal']['kind'] != 'gibbs':
+    # the thresholds t (sp.py:249): kept by the fused kernel
+    # (pbh_set_record_threshold), each chain's RandomState's last draw of
+    # the step, bit for bit
+    import oracle
+    ref = oracle.legacy_streams(sampler.spec, g['seeds'], t)[:, -1, :]
+    np.testing.assert_array_equal(np.asarray(summary.t), ref)
 
 
 @pytest.mark.gpu

@@ -229,6 +229,61 @@ def test_batched_sampler_reproduces_all_reference_chains(root):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('alpha', [31., 2.5, 1., 0.4])
+def test_device_gamma_equals_numpy_randomstate(alpha):
+  """pbh_legacy_draws: per chain NumPy's
+  RandomState(seed) drawing gibbs_linreg's cond_reg order -- standard_gamma
+  (alpha) on every third step, the legacy gauss otherwise -- on the device:
+  the same draws (NumPy's legacy_standard_gamma: Marsaglia-Tsang over the
+  polar gauss, the shape < 1 branch, shape 1 the exponential) and the same
+  generator state after them, across calls.  The device logs are within an
+  ulp of libm's, so the values agree to ~1e-15 relative and mostly exactly."""
+  from probayes_amd import Engine
+  from probayes_amd.spec import make_spec
+  n = 200
+  seeds = np.concatenate([[0, 1, 2 ** 32 - 1], np.arange(7, 7 + n - 3)])
+  eng = Engine(make_spec(1, target={'kind': 'diag_gauss', 'mu': np.zeros(1),
+                                    'sigma': np.ones(1)},
+                         proposal={'kind': 'gauss', 'loc': 0., 'scale': 1.},
+                         scores='hastings', pscale='log',
+                         tran={'kind': 'const', 'value': 1.0, 'sym': True}))
+  eng.init_chains(np.zeros((n, 1)))
+  eng.seed_legacy(seeds)
+  a = eng.legacy_draws(17, 0, 'linreg', alpha)
+  b = eng.legacy_draws(40, 17, 'linreg', alpha)
+  eng.close()
+  dev = np.concatenate([a, b])
+  ref = np.empty_like(dev)
+  for c, sd in enumerate(seeds):
+    rs = np.random.RandomState(int(sd))
+    for t in range(dev.shape[0]):
+      ref[t, c] = rs.standard_gamma(alpha) if t % 3 == 2 else rs.standard_normal()
+  rel = np.abs(dev - ref) / np.maximum(np.abs(ref), 1e-300)
+  assert rel.max() <= 4e-15, rel.max()
+  # exact for most; shape < 1 goes through pow (the device's within ~1 ulp
+  # of libm's)
+  assert np.mean(dev == ref) > (0.95 if alpha >= 1. else 0.8)
+
+
+@pytest.mark.gpu
+def test_batched_sampler_at_full_width_on_device_streams(root):
+  """The seeded linreg sampler at 65 536 chains: its RandomStates are drawn
+  on the device (no per-chain Python loop); the golden chains, placed among
+  the others, reproduce the reference's recorded chains."""
+  process, init, extra, kwds, keys, g, t = _facade(root)
+  n = 65536
+  seeds = np.arange(n, dtype=np.int64) + 10 ** 6
+  at = np.array([5, 40000, 65535])[:len(g['seeds'])]
+  seeds[at] = g['seeds'][:len(at)]
+  sm = process.sampler(init, extra, stop=t, chains=n, seeds=seeds, **kwds)
+  summary = process(process.walk(sm))
+  for i, k in enumerate(keys):
+    got = np.asarray(summary.v[k]).T[at]      # [T, N] -> [N, T]
+    want = g['v_x'][:len(at), :, i]
+    assert np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.)) <= 1e-12
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('vsets', [None, ((-1., -0.95), (1.3, 1.6), (0.4, 0.62))])
 def test_replay_priors_and_vset_bounds_match_oracle(vsets):
   """joint=False (no prior) and tight vsets the chains leave: the
