@@ -261,10 +261,9 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
   elif warmup:
     eng.run(warmup, steps_per_launch=warmup_spl or spl)
   barrier()
+  # the timed region: one library call (pbh_run_wait: the run and its wait)
   t0 = time.perf_counter()
-  eng.run(steps, steps_per_launch=spl, sync=False)
-  t1 = time.perf_counter()
-  eng.sync()
+  eng.run(steps, steps_per_launch=spl, sync=True)
   el = time.perf_counter() - t0
   kern_ms, launches = eng.last_run_ms()
   barrier()
@@ -273,7 +272,7 @@ def run_rank(eng, col, rank, world, chains_per_gpu, steps, warmup, spl, rng,
     server = eng.server_info()
     eng.stop_server()   # nothing else on this device waits behind it
   out = {'n': n, 'offset': offset, 'el': el, 'kern_ms': kern_ms,
-         'launches': launches, 'enqueue_s': t1 - t0, 'server': server}
+         'launches': launches, 'server': server}
   if col is not None:
     out['el'] = col.allreduce_max(el)
     if not gather:
@@ -311,7 +310,7 @@ def run_launched_rank(make_engine, col, rank, world, chains_per_gpu, steps,
   return {'chain_steps_per_s': float(chains_per_gpu) * world * steps / res['el'],
           'ms_per_step': res['el'] * 1e3 / steps,
           'events_us': kern_ms * 1e3, 'launches': launches,
-          'host_enqueue_us': res['enqueue_s'] * 1e6}
+          'host_us': (res['el'] - kern_ms / 1e3) * 1e6}
 
 
 def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup,
@@ -335,9 +334,12 @@ def run_replay_rank(make_engine, col, rank, world, chains_per_gpu, steps, warmup
   eng.seed_legacy(offset + np.arange(n))
   eng.alloc_trace(warmup + steps, 1)
   chunk = max(1, min(spl, steps))
-  # the stream buffer sized once for the largest generation (a growth inside
-  # the timed region would be a 100 MB-class hipMalloc there)
-  eng.reserve_replay(max(chunk, min(spl, warmup) if warmup else 1))
+  if os.environ.get('PBH_LEGACY_FUSED', '1') == '0':
+    # generation + REPLAY kernel: the stream buffer sized once for the
+    # largest generation (a growth inside the timed region would be a
+    # 100 MB-class hipMalloc there); the fused kernel (the default for this
+    # form) writes no stream, so nothing is reserved for it
+    eng.reserve_replay(max(chunk, min(spl, warmup) if warmup else 1))
 
   def advance(k):
     eng.legacy_run(k, steps_per_launch=chunk, sync=False)
@@ -492,10 +494,11 @@ def main():
         'timing': ('device stamps of the resident server command'
                    if res.get('server') and res['server'].get('commands')
                    else 'HIP events around the launches'),
-        # where the timed region's wall time went (rank 0): the host enqueue
-        # of the launches, the HIP-event time of the launches
-        'host_enqueue_us': res['enqueue_s'] * 1e6,
+        # where the timed region's wall time went: the device time of the
+        # launches / command (HIP events, or the server's stamps) and the
+        # rest (host call, submission, completion signalling)
         'events_us': kern_ms * 1e3,
+        'host_us': (el - kern_ms / 1e3) * 1e6,
         'lib_sha256': sha,
     }
     if collect_ms is not None:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define PBH_ABI_VERSION 5
+#define PBH_ABI_VERSION 6
 #define PBH_MAX_DIM 32
 
 #define PBH_OK 0
@@ -304,6 +304,9 @@ int pbh_alloc_trace(pbh_engine *eng, int64_t capacity, int32_t thin,
  * steps_per_launch bounds one kernel's fused step loop (0 = all).          */
 int pbh_run(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
 int pbh_sync(pbh_engine *eng);
+/* pbh_run + pbh_sync in one call (one host-to-library crossing: the
+ * synchronous walk of sp.py:281-295 for a batch of steps).                  */
+int pbh_run_wait(pbh_engine *eng, int64_t n_steps, int32_t steps_per_launch);
 /* flags = OR of enum pbh_collect; default PBH_COLLECT_MOMENTS.  With 0 the
  * kernels keep no running moments (no per-launch read-modify-write of them);
  * pbh_trace_stats then reduces the recorded trace on the device instead.   */
@@ -352,6 +355,10 @@ int pbh_reset_moments(pbh_engine *eng);
  * PBH_ESS_FFT=0); ess [d][N] on the host (may be NULL).  The result also
  * stays in the engine for pbh_rccl_allgather_stats.                         */
 int pbh_trace_ess(pbh_engine *eng, int64_t first, int64_t count, double *ess);
+/* The sum over chains of pbh_trace_ess's per-chain ESS, per dim: total[d]
+ * (cfg5's ESS is the min over dims of the summed per-chain
+ * ESS), reduced on the device -- d doubles cross to the host, not d N.      */
+int pbh_trace_ess_total(pbh_engine *eng, int64_t first, int64_t count, double *total);
 /* The same per-chain statistics reduced on the device from trace records
  * [first, first + count) (PD summate + expectation over a recorded trace,
  * pd_utils.py:332-411, pd.py:373-407, without copying the trace to the

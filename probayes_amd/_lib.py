@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('PBHIP_LIB', os.path.join(_HERE, 'libpbhip.so'))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 DRAWS_GAUSS, DRAWS_LINREG = 0, 1   # enum pbh_draws
 MAX_DIM = 32
 
@@ -102,6 +102,9 @@ SIGNATURES = {
                                        ctypes.c_int32, ctypes.c_int32]),
     'pbh_run': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),
     'pbh_sync': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_run_wait': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]),
+    'pbh_trace_ess_total': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64,
+                                           ctypes.c_int64, _dp]),
     'pbh_set_collect': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     'pbh_last_run_ms': (ctypes.c_int, [ctypes.c_void_p, _dp, _i64p]),
     'pbh_server_stop': (ctypes.c_int, [ctypes.c_void_p]),

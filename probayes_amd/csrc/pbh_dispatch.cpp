@@ -1185,6 +1185,30 @@ hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
   return hipGetLastError();
 }
 
+// The ESS total of one dim per workgroup: each of 1 024 threads sums the
+// chains c = t, t + 1 024, ... in order, then a fixed tree over the threads
+// (the same order every call: deterministic).
+__global__ __launch_bounds__(1024) void ess_total_kernel(const double *ess, int64_t n,
+                                                        double *total) {
+  __shared__ double part[1024];
+  const double *row = ess + (int64_t)blockIdx.x * n;
+  double acc = 0.0;
+  for (int64_t c = threadIdx.x; c < n; c += 1024) acc += row[c];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) total[blockIdx.x] = part[0];
+}
+
+hipError_t launch_ess_total(const double *ess, int64_t n, int32_t d, double *total,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(ess_total_kernel, dim3((unsigned)d), dim3(1024), 0, st, ess, n, total);
+  return hipGetLastError();
+}
+
 // The bm64 tables (pbh_device.h): sin(J 2 pi / 1024) and cos(J 2 pi / 1024),
 // J = 0..1023 (the first quadrant evaluated, the others by exact symmetry)
 // as four arrays of 32-bit words (sin lo, sin hi, cos lo, cos hi); then

@@ -59,6 +59,7 @@ struct pbh_engine {
   bool mt_odd = false;         // a stream may sit at an odd word (randint drew single words)
   bool rec_thr = false;        // pbh_set_record_threshold: keep pbh_legacy_run's thresholds
   double *thr = nullptr;       // [thr_steps][n] thresholds of the last pbh_legacy_run
+  double *ess_tot = nullptr;   // pbh_trace_ess_total's per-dim sums (PBH_MAX_DIM)
   size_t thr_alloc = 0;
   int64_t thr_steps = 0;
   int32_t *mt_pos = nullptr, *mt_has = nullptr, *mt_order = nullptr;
@@ -500,7 +501,7 @@ int pbh_destroy(pbh_engine *e) {
   free_trace(e);
   dfree(e->msum); dfree(e->msq); dfree(e->nacc);
   dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
-  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab); dfree(e->ess_list);
+  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab); dfree(e->ess_list); dfree(e->ess_tot);
   if (e->ess_host) (void)hipHostFree(e->ess_host);
   if (e->srv_cmd) (void)hipHostFree(e->srv_cmd);
   if (e->srv_done) (void)hipHostFree(e->srv_done);
@@ -1548,6 +1549,12 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   return PBH_OK;
 }
 
+int pbh_run_wait(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
+  const int rc = pbh_run(e, n_steps, steps_per_launch);
+  if (rc) return rc;
+  return pbh_sync(e);
+}
+
 int pbh_set_record_threshold(pbh_engine *e, int32_t on) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
   e->rec_thr = on != 0;
@@ -1598,6 +1605,20 @@ int pbh_legacy_draws(pbh_engine *e, int64_t n_steps, int64_t step0, int32_t kind
   dfree(dout);
   if (err != hipSuccess) return fail(PBH_ERR_HIP, "pbh_legacy_draws: %s", hipGetErrorString(err));
   return PBH_OK;
+}
+
+// The engine stream's completion, as pbh_sync waits for it: polled for up to
+// 2 ms (PBH_SYNC, spin_sync), then a blocking wait.  A blocking
+// hipStreamSynchronize wakes ~10-50 us after a short kernel ends.
+static hipError_t stream_wait(pbh_engine *e) {
+  if (!e->spin_sync) return hipStreamSynchronize(e->stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t q;
+  while ((q = hipStreamQuery(e->stream)) == hipErrorNotReady) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000))
+      return hipStreamSynchronize(e->stream);
+  }
+  return q;
 }
 
 int pbh_sync(pbh_engine *e) {
@@ -2011,11 +2032,33 @@ int pbh_trace_ess(pbh_engine *e, int64_t first, int64_t count, double *ess) {
     }
     HIP_TRY(hipMemcpyAsync(e->ess_host, e->ess, dn * sizeof(double), hipMemcpyDeviceToHost,
                            e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(stream_wait(e));
     std::memcpy(ess, e->ess_host, dn * sizeof(double));
-  } else {
-    HIP_TRY(hipStreamSynchronize(e->stream));
   }
+  return PBH_OK;
+}
+
+int pbh_trace_ess_total(pbh_engine *e, int64_t first, int64_t count, double *total) {
+  if (check_ptr(e, "engine") || check_ptr(total, "total")) return PBH_ERR_ARG;
+  // the per-chain ESS on the device (no copy), then the per-dim sums
+  if (const int rc = pbh_trace_ess(e, first, count, nullptr)) return rc;
+  const int d = e->d;
+  if (!e->ess_host || e->ess_host_len < d) {
+    if (e->ess_host) (void)hipHostFree(e->ess_host);
+    e->ess_host = nullptr;
+    e->ess_host_len = 0;
+    HIP_TRY(hipHostMalloc(&e->ess_host, d * sizeof(double), hipHostMallocDefault));
+    e->ess_host_len = d;
+  }
+  // the totals land in the scalar scratch (d doubles, allocated lazily)
+  if (!e->ess_tot) {
+    if (const int rc = dalloc(e->ess_tot, PBH_MAX_DIM)) return rc;
+  }
+  HIP_TRY(pbh::launch_ess_total(e->ess, e->n, d, e->ess_tot, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->ess_host, e->ess_tot, d * sizeof(double), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(stream_wait(e));
+  std::memcpy(total, e->ess_host, d * sizeof(double));
   return PBH_OK;
 }
 

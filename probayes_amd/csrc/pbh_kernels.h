@@ -211,6 +211,10 @@ hipError_t launch_trace_expectation(const double *tx, const double *tlp,
 hipError_t launch_trace_ess(const double *tx, int64_t n, int32_t d,
                             int64_t first, int64_t count, double *ess,
                             hipStream_t st, int fft, int32_t *list);
+// total[k] = sum over chains of ess[k][c] (one workgroup per dim, a fixed
+// summation order)
+hipError_t launch_ess_total(const double *ess, int64_t n, int32_t d, double *total,
+                            hipStream_t st);
 // Host: the bm64 LDS tables (kBm64Doubles doubles, long-double accurate).
 void bm64_tables(double *out);
 // the legacy generator's log table (pbh_legacy.hip log_leg): 129 rows of

@@ -107,6 +107,7 @@ class Engine:
     # getattr and c_int64 boxing per call were ~1 us of a 20-step run's ~35)
     lib = _lib.load()
     self._fn_run, self._fn_sync = lib.pbh_run, lib.pbh_sync
+    self._fn_run_wait = lib.pbh_run_wait
     _LIVE.add(self)
     self.device = device
     self.n = 0
@@ -288,11 +289,11 @@ class Engine:
     self.debug = bool(debug)
 
   def run(self, n_steps, steps_per_launch=0, sync=True):
-    rc = self._fn_run(self._h, int(n_steps), int(steps_per_launch))
+    # sync: one library call (pbh_run_wait) instead of pbh_run + pbh_sync
+    fn = self._fn_run_wait if sync else self._fn_run
+    rc = fn(self._h, int(n_steps), int(steps_per_launch))
     if rc:
-      _lib.raise_status('pbh_run', rc)
-    if sync:
-      self.sync()
+      _lib.raise_status('pbh_run_wait' if sync else 'pbh_run', rc)
 
   def legacy_run(self, n_steps, steps_per_launch=0, sync=True):
     """legacy_replay(n) + run(n) in one kernel per launch (the draws go
@@ -565,6 +566,15 @@ class Engine:
     _lib.call('pbh_trace_ess', self._h, _c.c_int64(int(first)),
               _c.c_int64(int(count)), _dp(out))
     return out.T   # a [N, d] view of the [d][N] result (no 2-D transpose copy)
+
+  def trace_ess_total(self, first=0, count=None):
+    """Per dim, the sum over chains of trace_ess (reduced on the device):
+    [d]."""
+    count = self.trace_len() - first if count is None else count
+    out = np.empty(self.dim)
+    _lib.call('pbh_trace_ess_total', self._h, _c.c_int64(int(first)),
+              _c.c_int64(int(count)), _dp(out))
+    return out
 
   def trace_expectation(self, first=0, count=None, exponent=None):
     """PD.expectation (pd.py:373-405) of the summary of trace records

@@ -28,8 +28,7 @@ for _ in range(5):
   eng.run(1)
 for rep in range(10):
   t0 = time.perf_counter()
-  eng.run(steps, sync=False)
-  eng.sync()
+  eng.run(steps)   # pbh_run_wait: one call
   wall = (time.perf_counter() - t0) * 1e6
   ms, _ = eng.last_run_ms()
   q, a, b = eng.server_stamps()
