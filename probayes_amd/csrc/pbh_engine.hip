@@ -137,17 +137,18 @@ struct pbh_engine {
   int64_t srv_idle_ms = 1000;      // PBH_SERVER_IDLE_MS: the kernel's idle exit
   pbh::SrvCmd *srv_cmd = nullptr;  // pinned, fine-grained
   pbh::SrvDone *srv_done = nullptr;
-  pbh::SrvCmd *srv_mail = nullptr;   // device memory: workgroup 0's relay
+  pbh::SrvCmd *srv_mail = nullptr;   // the device mailbox the workgroups poll
   int32_t srv_done_len = 0;
-  // the command protocol (KArgs.srv_mode): bit 0 direct -- srv_mail is
-  // fine-grained device memory the host writes through srv_wmail (its host
-  // mapping) and every workgroup polls; bit 1 single -- one completion word
-  // srv_fin (pinned host), written by the last workgroup (counter srv_cnt)
-  int32_t srv_mode = 0;
+  // the command protocol (KArgs.srv_mode): 1 direct (the default) --
+  // srv_mail is fine-grained device memory the host writes through srv_wmail
+  // (its host mapping) and every workgroup polls; 0 relay -- workgroup 0
+  // polls the pinned host block srv_cmd and copies each command into
+  // srv_mail.  Direct needs a host mapping whose stores the device sees: the
+  // first launch probes it (srv_probed) and falls back to the relay.
+  int32_t srv_mode = 1;
+  bool srv_probed = false;
   bool srv_mail_fine = false;        // srv_mail came from the fine-grained pool
   pbh::SrvCmd *srv_wmail = nullptr;
-  uint32_t *srv_cnt = nullptr;
-  uint32_t *srv_fin = nullptr;
   // srv_last: the last submit (or launch) -- never moved forward at a wait:
   // a command completes after its submit, and each workgroup's idle timer
   // starts at its completion, so idle measured from the submit is an upper
@@ -280,20 +281,13 @@ bool srv_all_done(const pbh_engine *e, uint32_t seq) {
 int srv_wait(pbh_engine *e, uint32_t seq, bool ok_if_ended) {
   const auto t0 = srv_clk::now();
   int32_t w = 0;
-  const bool single = (e->srv_mode & 2) != 0;
   for (uint64_t it = 1;; ++it) {
-    if (single) {   // one word, written once every workgroup is done
-      if (__atomic_load_n(e->srv_fin, __ATOMIC_ACQUIRE) == seq) return PBH_OK;
-    } else {
-      w = srv_first_pending(e, seq, w);
-      if (w == e->srv_wgs) return PBH_OK;
-    }
+    w = srv_first_pending(e, seq, w);
+    if (w == e->srv_wgs) return PBH_OK;
     if ((it & 4095) == 0) {
       const auto el = srv_clk::now() - t0;
       if (el > std::chrono::milliseconds(1) && srv_kernel_ended(e)) {
-        if ((single ? __atomic_load_n(e->srv_fin, __ATOMIC_ACQUIRE) == seq
-                    : srv_all_done(e, seq)) || ok_if_ended)
-          return PBH_OK;
+        if (srv_all_done(e, seq) || ok_if_ended) return PBH_OK;
         // the kernel left without the command (some workgroups may have run
         // it): the server is gone -- the next eligible run relaunches -- and
         // the chain state is unusable until replaced
@@ -334,18 +328,54 @@ int srv_stop(pbh_engine *e) {
   if (!srv_kernel_ended(e)) {
     const uint32_t q = ++e->srv_seq;
     srv_write(e, 0u, pbh::srv_arg(0, 0u, 0u, pbh::kSrvExit, q), q);
-    // (single: the exit is not counted; every workgroup leaves on it and the
-    // stream's completion below is the acknowledgement)
-    if (!(e->srv_mode & 2)) {
-      const int rc2 = srv_wait(e, q, true);
-      if (!rc) rc = rc2;
-    }
+    const int rc2 = srv_wait(e, q, true);
+    if (!rc) rc = rc2;
   }
   const hipError_t err = hipStreamSynchronize(e->stream);
   e->srv_active = false;
   if (!rc && err != hipSuccess)
     rc = fail(PBH_ERR_HIP, "sampling server exit: %s", hipGetErrorString(err));
   return rc;
+}
+
+// the fine-grained device mailbox and the host's mapping of it (direct)
+int srv_alloc_fine(pbh_engine *e) {
+  hipError_t err = hipExtMallocWithFlags((void **)&e->srv_mail, sizeof(pbh::SrvCmd),
+                                         hipDeviceMallocFinegrained);
+  if (err != hipSuccess) {
+    e->srv_mail = nullptr;
+    return fail(PBH_ERR_HIP, "server mailbox: %s", hipGetErrorString(err));
+  }
+  e->srv_mail_fine = true;
+  hipPointerAttribute_t at{};
+  err = hipPointerGetAttributes(&at, e->srv_mail);
+  e->srv_wmail = static_cast<pbh::SrvCmd *>(err == hipSuccess ? at.hostPointer : nullptr);
+  if (!e->srv_wmail) {
+    dfree(e->srv_mail);
+    return fail(PBH_ERR_UNSUPPORTED, "server mailbox: no host mapping");
+  }
+  return PBH_OK;
+}
+
+// direct commands work here: the mailbox has a host mapping, and a pattern
+// stored through it reads back from the device (a copy engine read of the
+// device memory); otherwise the relay form serves
+int srv_probe_direct(pbh_engine *e) {
+  dfree(e->srv_mail);
+  if (const int rc = srv_alloc_fine(e)) return rc;
+  const uint32_t pat[4] = {0x5eed1234u, 0x0badf00du, 0x600df00du, 0xfeedfaceu};
+  volatile uint32_t *w = reinterpret_cast<volatile uint32_t *>(e->srv_wmail);
+  for (int i = 0; i < 4; ++i) w[i] = pat[i];
+  __builtin_ia32_sfence();
+  uint32_t back[4] = {0, 0, 0, 0};
+  const hipError_t err = hipMemcpy(back, e->srv_mail, sizeof back, hipMemcpyDeviceToHost);
+  if (err != hipSuccess || std::memcmp(back, pat, sizeof back) != 0) {
+    (void)hipGetLastError();
+    dfree(e->srv_mail);
+    e->srv_wmail = nullptr;
+    return fail(PBH_ERR_UNSUPPORTED, "server mailbox: host stores not seen by the device");
+  }
+  return PBH_OK;
 }
 
 int srv_launch(pbh_engine *e, pbh::KArgs k) {
@@ -371,41 +401,27 @@ int srv_launch(pbh_engine *e, pbh::KArgs k) {
     }
     e->srv_done_len = wgs;
   }
-  const bool direct = (e->srv_mode & 1) != 0, single = (e->srv_mode & 2) != 0;
+  if (!e->srv_probed) {   // direct: a host mapping whose stores the device sees
+    e->srv_probed = true;
+    if ((e->srv_mode & 1) && srv_probe_direct(e) != PBH_OK) e->srv_mode &= ~1;
+  }
+  const bool direct = (e->srv_mode & 1) != 0;
   if (e->srv_mail && direct != e->srv_mail_fine) dfree(e->srv_mail);
   if (!e->srv_mail) {
-    err = direct ? hipExtMallocWithFlags((void **)&e->srv_mail, sizeof(pbh::SrvCmd),
-                                         hipDeviceMallocFinegrained)
-                 : hipMalloc((void **)&e->srv_mail, sizeof(pbh::SrvCmd));
-    if (err != hipSuccess) {
-      e->srv_mail = nullptr;
-      return fail(PBH_ERR_HIP, "server mailbox: %s", hipGetErrorString(err));
-    }
-    e->srv_mail_fine = direct;
-    e->srv_wmail = nullptr;
-    if (direct) {   // the host's mapping of the mailbox
-      hipPointerAttribute_t at{};
-      HIP_TRY(hipPointerGetAttributes(&at, e->srv_mail));
-      e->srv_wmail = static_cast<pbh::SrvCmd *>(at.hostPointer ? at.hostPointer
-                                                               : (void *)e->srv_mail);
-    }
-  }
-  if (single && !e->srv_cnt) {
-    if (const int rc = dalloc(e->srv_cnt, 16)) return rc;
-  }
-  if (single && !e->srv_fin) {
-    err = hipHostMalloc((void **)&e->srv_fin, 64, hipHostMallocCoherent);
-    if (err != hipSuccess) {
-      e->srv_fin = nullptr;
-      return fail(PBH_ERR_HIP, "server completion word: %s", hipGetErrorString(err));
+    if (direct) {
+      if (const int rc = srv_alloc_fine(e)) return rc;
+    } else {
+      err = hipMalloc((void **)&e->srv_mail, sizeof(pbh::SrvCmd));
+      if (err != hipSuccess) {
+        e->srv_mail = nullptr;
+        return fail(PBH_ERR_HIP, "server mailbox: %s", hipGetErrorString(err));
+      }
+      e->srv_mail_fine = false;
+      e->srv_wmail = nullptr;
     }
   }
   // the previous server (if any) has ended: sequence numbers restart
   HIP_TRY(hipMemsetAsync(e->srv_mail, 0, sizeof(pbh::SrvCmd), e->stream));
-  if (single) {
-    HIP_TRY(hipMemsetAsync(e->srv_cnt, 0, 16 * sizeof(uint32_t), e->stream));
-    __atomic_store_n(e->srv_fin, 0u, __ATOMIC_RELEASE);
-  }
   // direct: the host writes the mailbox from the first command on, outside
   // the stream's order -- the zeroing above must have run by then
   if (direct) HIP_TRY(hipStreamSynchronize(e->stream));
@@ -413,16 +429,13 @@ int srv_launch(pbh_engine *e, pbh::KArgs k) {
   std::memset(e->srv_cmd, 0, sizeof(pbh::SrvCmd));
   std::atomic_thread_fence(std::memory_order_seq_cst);
   e->srv_seq = 0;
-  void *dcmd = nullptr, *ddone = nullptr, *dfin = nullptr;
+  void *dcmd = nullptr, *ddone = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dcmd, e->srv_cmd, 0));
   HIP_TRY(hipHostGetDevicePointer(&ddone, e->srv_done, 0));
-  if (single) HIP_TRY(hipHostGetDevicePointer(&dfin, e->srv_fin, 0));
   k.srv_cmd = dcmd;
   k.srv_done = ddone;
   k.srv_mail = e->srv_mail;
   k.srv_mode = e->srv_mode;
-  k.srv_cnt = e->srv_cnt;
-  k.srv_fin = dfin;
   k.srv_idle = e->srv_idle_ms * 100000;   // 10 ns ticks
   err = pbh::launch_mh_server(k, e->stream, &wgs, false);
   if (err != hipSuccess) return fail(PBH_ERR_HIP, "server launch: %s", hipGetErrorString(err));
@@ -507,10 +520,9 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *gf = std::getenv("PBH_GMM_FULL")) e->gmm_full = std::atoi(gf) != 0;
   if (const char *pf = std::getenv("PBH_PAIR_FULL")) e->pair_full = std::atoi(pf) != 0;
   if (const char *sv = std::getenv("PBH_SERVER")) e->srv_enabled = sv[0] == '1';
-  // PBH_SERVER_DIRECT=1: commands written straight into device memory (no
-  // relay); PBH_SERVER_SINGLE=1: one completion word (tools/ubench/mailbox_rtt)
-  if (const char *sd = std::getenv("PBH_SERVER_DIRECT")) e->srv_mode = (e->srv_mode & ~1) | (sd[0] == '1' ? 1 : 0);
-  if (const char *ss = std::getenv("PBH_SERVER_SINGLE")) e->srv_mode = (e->srv_mode & ~2) | (ss[0] == '1' ? 2 : 0);
+  // PBH_SERVER_DIRECT=0: the relay form (workgroup 0 polls the host block);
+  // the default writes commands straight into device memory
+  if (const char *sd = std::getenv("PBH_SERVER_DIRECT")) e->srv_mode = sd[0] == '1' ? 1 : 0;
   if (const char *si = std::getenv("PBH_SERVER_IDLE_MS"))
     e->srv_idle_ms = std::max<int64_t>(1, std::min<int64_t>(10000, std::atoll(si)));
   if (const char *ef = std::getenv("PBH_ESS_FFT")) e->ess_fft = std::atoi(ef);
@@ -569,8 +581,6 @@ int pbh_destroy(pbh_engine *e) {
   if (e->srv_cmd) (void)hipHostFree(e->srv_cmd);
   if (e->srv_done) (void)hipHostFree(e->srv_done);
   dfree(e->srv_mail);
-  dfree(e->srv_cnt);
-  if (e->srv_fin) (void)hipHostFree(e->srv_fin);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->stream) (void)hipStreamDestroy(e->stream);

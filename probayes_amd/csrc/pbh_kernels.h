@@ -135,17 +135,13 @@ struct KArgs {
   // memory, SrvCmd / SrvDone), and the idle exit in 10 ns ticks
   void *srv_cmd;
   void *srv_done;
-  void *srv_mail;     // device copy of the command (SrvCmd), relayed by workgroup 0
+  void *srv_mail;     // the device mailbox of the command (SrvCmd)
   int64_t srv_idle;
-  // srv_mode bit 0 (direct): the host writes each command straight into
-  // srv_mail (fine-grained device memory through the host's mapping of it)
-  // and every workgroup polls it (no relay); bit 1 (single): the last
-  // workgroup to finish a command -- by the device counter srv_cnt -- writes
-  // seq to the one host word srv_fin (the per-workgroup SrvDone stamps are
-  // still written, before the counter)
+  // srv_mode bit 0 (direct, the default): the host writes each command
+  // straight into srv_mail (fine-grained device memory through the host's
+  // mapping of it) and every workgroup polls it; 0 (relay): workgroup 0
+  // polls srv_cmd and copies each command into srv_mail for the others
   int32_t srv_mode;
-  uint32_t *srv_cnt;
-  void *srv_fin;
   // ---- moments ----
   int32_t moments;     // 1: accumulate sum / sumsq / n_acc (pbh_set_collect)
   double *msum, *msq;

@@ -1813,7 +1813,7 @@ void mh_pair_kernel(KArgs a) {
           SrvCmd *const mail = reinterpret_cast<SrvCmd *>(a.srv_mail);
           SrvDone *const donep = reinterpret_cast<SrvDone *>(a.srv_done) + blockIdx.x;
           const bool poller = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == 0;
-          const bool direct = (a.srv_mode & 1) != 0, single = (a.srv_mode & 2) != 0;
+          const bool direct = (a.srv_mode & 1) != 0;
           // the one host poller (direct: none -- the host writes the mailbox)
           const bool relay = blockIdx.x == 0 && !direct;
           uint32_t seen = 0u;
@@ -1880,20 +1880,6 @@ void mh_pair_kernel(KArgs a) {
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               __builtin_amdgcn_s_waitcnt(0);   // the stamps before the seq
               __hip_atomic_store(&donep->seq, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              if (single) {
-                // after every wave's stores and this workgroup's stamps: the
-                // workgroup that completes the count (q commands x workgroups
-                // since the launch; exit commands are not counted) tells the
-                // host through one word
-                __builtin_amdgcn_s_waitcnt(0);
-                if (threadIdx.x == 0) {
-                  const uint32_t old = __hip_atomic_fetch_add(a.srv_cnt, 1u, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-                  if (old + 1u == q * gridDim.x)
-                    __hip_atomic_store(reinterpret_cast<uint32_t *>(a.srv_fin), q,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-              }
             }
             seen = q;
           }

@@ -1563,211 +1563,9 @@ hipError_t launch_legacy_mh_t(const LegacyArgs &la, const KArgs &a, hipStream_t 
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// Pipelined fused REPLAY (legacy_mh_pipe_kernel, round 6; PBH_LEGACY_PIPE=1
-// selects it).  65 536 chains at one chain per lane are exactly one
-// wavefront per SIMD, and legacy_mh_kernel's lone wave is latency-bound
-// (VALU active ~0.35, dependency waits ~0.34 of its cycles): the generator's
-// lockstep attempts, the polar method's log / division / square root and the
-// step's density form one serial instruction stream per lane.  Here each
-// chain has TWO lanes in two wavefronts of one workgroup (512 threads = 256
-// chains, one workgroup per CU, so two waves per SIMD):
-//  * producer waves (threads 256..511) own the Mt4 state and window: the
-//    twist rounds, the refills (tempering + conversion), the lockstep polar
-//    ATTEMPTS, and the threshold double; each step's accepted (x1, x2) pairs
-//    and threshold go into slot s & 1 of an LDS ring;
-//  * consumer waves (threads 0..255) run mh_body unchanged with RingDraws as
-//    the draw source: the pairs' transcendental part (polar_pair: the same
-//    operations, the same order, the cached deviate kept here) and the
-//    REPLAY step, density, score and trace.
-// One workgroup barrier per step hands slot s & 1 over (the producer fills
-// step s + 1 while the consumer runs step s; both sides pass exactly n_steps
-// barriers).  The values, their order and the legacy state written back are
-// legacy_mh_kernel's, so streams, chains and traces are bit-identical
-// (tests/test_gpu_legacy_fused.py runs both forms).  LDS: the windows at
-// H = 8 (64 KB) plus two ring slots of (d + 1) / 2 pairs + a threshold per
-// lane (45 KB at d = 10).
-// ---------------------------------------------------------------------------
-template <bool NORMAL, int D>
-struct PipeRing {
-  static constexpr int NP = (D + 1) / 2;   // pairs per step, at most
-  // bytes of one slot: NORMAL: [NP][256] double2 pairs, then [256] thresholds;
-  // raw: [D + 1][256] doubles (the threshold last)
-  static constexpr int kPairBytes = NORMAL ? NP * kBlockLegacy * 16 : D * kBlockLegacy * 8;
-  static constexpr int kSlotBytes = kPairBytes + kBlockLegacy * 8;
-  __device__ __forceinline__ static double2 *pairs(char *ring, int s) {
-    return reinterpret_cast<double2 *>(ring + (s & 1) * kSlotBytes);
-  }
-  __device__ __forceinline__ static double *raw(char *ring, int s) {
-    return reinterpret_cast<double *>(ring + (s & 1) * kSlotBytes);
-  }
-  __device__ __forceinline__ static double *thr(char *ring, int s) {
-    return reinterpret_cast<double *>(ring + (s & 1) * kSlotBytes + kPairBytes);
-  }
-};
-
-template <int H, bool NORMAL, int D>
-struct RingDraws {
-  using R = PipeRing<NORMAL, D>;
-  using M = Mt4<H, true>;
-  char *ring;
-  const double *s_lg;
-  double gauss;
-  int has;
-  double *thr_out;   // [n_steps][n] thresholds (pbh_set_record_threshold) or nullptr
-  int64_t n;
-
-  __device__ __forceinline__ void begin() { __builtin_amdgcn_s_waitcnt(0); }
-
-  // LegacyDraws::normals on the producer's accepted pairs (J0 = 1: the
-  // cached deviate leads)
-  template <int J0>
-  __device__ __forceinline__ void normals(const double2 *st, double (&r)[D]) {
-    constexpr int need = (D - J0 + 1) / 2, half = (D - J0) & 1, nfull = need - half;
-    if constexpr (J0 == 1) {
-      r[0] = gauss;
-      has = 0;
-      gauss = 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < nfull; ++k) {
-      double g0, g1;
-      polar_pair<M>(st, k, s_lg, g0, g1);
-      r[J0 + 2 * k] = g0;
-      r[J0 + 2 * k + 1] = g1;
-    }
-    if constexpr (half != 0) {
-      double g0, g1;
-      polar_pair<M>(st, nfull, s_lg, g0, g1);
-      r[J0 + 2 * nfull] = g0;
-      gauss = g1;   // cached for the next draw (odd d)
-      has = 1;
-    }
-  }
-
-  template <int DD>
-  __device__ __forceinline__ void draws(const KArgs &, int s, int64_t cc, double (&r)[DD],
-                                        double &thr) {
-    static_assert(DD == D, "one dimension per instantiation");
-    __syncthreads();   // the producer filled slot s & 1 (and we left slot s - 1)
-    if constexpr (NORMAL) {
-      has = __builtin_amdgcn_readfirstlane(has);   // the same in every lane
-      if (has) normals<1>(R::pairs(ring, s), r);
-      else normals<0>(R::pairs(ring, s), r);
-    } else {
-      const double *rw = R::raw(ring, s);
-#pragma unroll
-      for (int k = 0; k < D; ++k) r[k] = rw[k * kBlockLegacy + threadIdx.x];
-    }
-    thr = R::thr(ring, s)[threadIdx.x];
-    if (thr_out) thr_out[(int64_t)s * n + cc] = thr;
-  }
-};
-
-// the producer side: every step's pairs (or raw doubles) and threshold into
-// the ring, one barrier per step (after the slot is full)
-template <int D, int H, bool NORMAL>
-__device__ __forceinline__ void pipe_produce(const LegacyArgs &la, int64_t c, int t, w4 *s_lw,
-                                             char *ring) {
-  using R = PipeRing<NORMAL, D>;
-  using M = Mt4<H, true>;
-  M m;
-  m.key = reinterpret_cast<w4 *>(la.key);
-  m.n = la.n;
-  m.c = c;
-  m.init(la.pos[c], s_lw + t);
-  int has = NORMAL ? la.has_gauss[c] : 0;
-  __builtin_amdgcn_s_waitcnt(0);   // every entry load before the loop (see legacy_gen_body)
-  has = __builtin_amdgcn_readfirstlane(has);
-  const int nsteps = (int)la.n_steps;
-  for (int s = 0; s < nsteps; ++s) {
-    m.maintain();   // wave-uniform: every active lane is here
-    if constexpr (NORMAL) {
-      const int j0 = has;
-      polar_attempts(m, (D - j0 + 1) / 2, R::pairs(ring, s), t);
-      has = (D - j0) & 1;   // the consumer caches the last pair's second deviate
-    } else {
-      double *rw = R::raw(ring, s);
-#pragma unroll
-      for (int k = 0; k < D; ++k) rw[k * kBlockLegacy + t] = m.next_double();
-    }
-    R::thr(ring, s)[t] = m.next_double();   // the MH threshold
-    // this step's window prefetch complete (vmcnt(0), as legacy_gen_body)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();   // slot s & 1 is full
-  }
-  la.pos[c] = m.packed();
-}
-
-template <int D, int H, bool NORMAL, int TGT, int PROP>
-__global__ __launch_bounds__(2 * kBlockLegacy) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void legacy_mh_pipe_kernel(LegacyArgs la, KArgs a) {
-  static_assert(kBlockLegacy == kBlock, "mh_body's chain index");
-  extern __shared__ w4 s_lw[];   // the producers' windows [2H][256] quads, then the ring
-  __shared__ double s_lg[kLegLogDoubles];
-  for (int i = threadIdx.x; i < kLegLogDoubles; i += 2 * kBlockLegacy) s_lg[i] = la.lgtab[i];
-  __syncthreads();
-  char *const ring = reinterpret_cast<char *>(s_lw + 2 * H * kBlockLegacy);
-  const int t = threadIdx.x & (kBlockLegacy - 1);
-  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + t;
-  // the wave's role as a scalar: the branch and the barriers inside it are
-  // scalar control flow, never a lane-masked (linearised) region
-  const bool producer =
-      __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= kBlockLegacy;
-  // lanes past the last chain leave at once on both sides (a wave's barrier
-  // needs only its live lanes; a wave with none has ended, and barriers
-  // count live waves only)
-  if (c >= la.n) return;
-  if (producer) {
-    pipe_produce<D, H, NORMAL>(la, c, t, s_lw, ring);
-    return;
-  }
-  RingDraws<H, NORMAL, D> src{ring, s_lg, la.gauss[c], la.has_gauss[c], la.thr, la.n};
-  mh_body<D, PBH_RNG_REPLAY, TGT, PROP>(a, src, nullptr, false);
-  la.gauss[c] = src.gauss;
-  la.has_gauss[c] = src.has;
-}
-
-template <int D, bool NORMAL, int TGT, int PROP>
-hipError_t launch_legacy_mh_pipe_t(const LegacyArgs &la, const KArgs &a, hipStream_t s) {
-  constexpr int H = 8;
-  const void *fn = reinterpret_cast<const void *>(&legacy_mh_pipe_kernel<D, H, NORMAL, TGT, PROP>);
-  const size_t lds = (size_t)2 * H * kBlockLegacy * sizeof(uint4) +
-                     2 * (size_t)PipeRing<NORMAL, D>::kSlotBytes;
-  static const hipError_t attr =
-      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (attr != hipSuccess) return attr;
-  const dim3 grid((unsigned)((la.n + kBlockLegacy - 1) / kBlockLegacy)), block(2 * kBlockLegacy);
-  LaunchEvents &ev = launch_events();
-  if (ev.start || ev.stop)
-    (void)hipExtLaunchKernelGGL((legacy_mh_pipe_kernel<D, H, NORMAL, TGT, PROP>), grid, block,
-                                (uint32_t)lds, s, ev.start, ev.stop, 0u, la, a);
-  else
-    hipLaunchKernelGGL((legacy_mh_pipe_kernel<D, H, NORMAL, TGT, PROP>), grid, block, lds, s,
-                       la, a);
-  ev.start = nullptr;
-  return hipGetLastError();
-}
-
-bool legacy_pipe_on() {
-  static const bool on = [] {
-    const char *p = std::getenv("PBH_LEGACY_PIPE");
-    return p && p[0] == '1';
-  }();
-  return on;
-}
-
 template <int D>
 hipError_t launch_legacy_mh_d(const LegacyArgs &la, const KArgs &a, hipStream_t s) {
   constexpr int H = D <= 12 ? 16 : 8;   // the window while the stage leaves room
-  if (legacy_pipe_on()) {
-    if (la.normal) {
-      if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS)   // cfg2's form
-        return launch_legacy_mh_pipe_t<D, true, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>(la, a, s);
-      return launch_legacy_mh_pipe_t<D, true, 0, 0>(la, a, s);
-    }
-    return launch_legacy_mh_pipe_t<D, false, 0, 0>(la, a, s);
-  }
   if (la.normal) {
     if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS)   // cfg2's form
       return launch_legacy_mh_t<D, H, true, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>(la, a, s);
