@@ -179,7 +179,16 @@ const char *pbh_last_error(void);
 int pbh_abi_version(void);
 int pbh_device_count(int *count);
 int pbh_create(int device, pbh_engine **out);
+/* Destroys the engine.  Its device buffers, stream and events (drained) stay
+ * in a process-wide cache for the next engine of the same device (one
+ * engine per SP.sampler call); PBH_CACHE_MB bounds the cached buffers
+ * (default 32 768, 0: no cache).                                            */
 int pbh_destroy(pbh_engine *eng);
+/* Frees every cached buffer and stream (an allocation that fails does this
+ * itself and retries).                                                       */
+int pbh_cache_release(void);
+/* Cached (idle) bytes, and allocations served from / missed in the cache.  */
+int pbh_cache_info(int64_t *idle_bytes, int64_t *hits, int64_t *misses);
 
 /* ---- model ------------------------------------------------------------- */
 int pbh_set_model(pbh_engine *eng, const pbh_model *model);
@@ -297,7 +306,10 @@ int pbh_legacy_draws(pbh_engine *eng, int64_t n_steps, int64_t step0, int32_t ki
 
 /* ---- running (SP.walk / sample_generator: sp.py:281-295, sp_utils.py:8-16) */
 /* Device trace ring for the next runs: every thin-th step is recorded.
- * debug = 1 also records proposals p_x, p_p and the score s.               */
+ * debug = 1 also records proposals p_x, p_p and the score s; OR-ed with
+ * PBH_TRACE_NOFILL the records are not zero-filled (the caller's next run
+ * writes every one of them).                                                */
+enum { PBH_TRACE_NOFILL = 0x100 };
 int pbh_alloc_trace(pbh_engine *eng, int64_t capacity, int32_t thin,
                     int32_t debug);
 /* Launches n_steps chain-steps on the engine stream (asynchronous);

@@ -76,6 +76,8 @@ SIGNATURES = {
     'pbh_device_count': (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     'pbh_create': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     'pbh_destroy': (ctypes.c_int, [ctypes.c_void_p]),
+    'pbh_cache_release': (ctypes.c_int, []),
+    'pbh_cache_info': (ctypes.c_int, [ctypes.POINTER(ctypes.c_int64)] * 3),
     'pbh_set_model': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PbhModel)]),
     'pbh_set_proposal': (ctypes.c_int, [ctypes.c_void_p,
                                         ctypes.POINTER(PbhProposal)]),

@@ -16,6 +16,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <map>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/pbhip.h"
@@ -28,6 +31,7 @@ struct pbh_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  unsigned ev_flags = 0;   // the events' hipEventCreateWithFlags flags
   // model / proposal / gibbs (device constant blocks)
   bool has_model = false, has_prop = false, has_gibbs = false;
   int d = 0;
@@ -196,17 +200,134 @@ int fail(int code, const char *fmt, ...) {
       return fail(PBH_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
   } while (0)
 
+// ---------------------------------------------------------------------------
+// Engine resource cache.  The device buffers, stream and events of a
+// destroyed engine are kept (its stream drained first) for the next engine on
+// the same device: a seeded SP.sampler builds one engine per call, and at
+// 65 536 chains the hipMalloc / hipFree of its state and trace buffers and
+// the stream setup were ~7 ms around an 11.6 ms run
+// (profiles/r06_facade/setup_probe.jsonl).  Only buffers of destroyed
+// engines enter the cache, so nothing in it has work in flight; a live
+// engine's reallocations free as before.  Buffers are reused at exactly
+// their size (engines of one shape ask for the same sizes).  Bounded by
+// PBH_CACHE_MB (default 32 768 of the 288 GB; 0 disables it); an allocation
+// that fails empties the cache and retries; pbh_cache_release empties it.
+// ---------------------------------------------------------------------------
+struct ResCache {
+  std::mutex mu;
+  std::unordered_map<void *, size_t> live;              // dalloc'd buffers: bytes
+  std::multimap<std::pair<int, size_t>, void *> idle;   // (device, bytes) -> buffer
+  size_t idle_bytes = 0, cap = 0;
+  struct Strm { int device; unsigned flags; hipStream_t s; hipEvent_t e0, e1; };
+  std::vector<Strm> streams;
+  int64_t hits = 0, misses = 0;
+};
+ResCache &res_cache() {
+  static ResCache *c = [] {   // never destroyed: engines may outlive statics
+    ResCache *r = new ResCache();
+    size_t mb = 32768;
+    if (const char *m = std::getenv("PBH_CACHE_MB")) mb = std::strtoull(m, nullptr, 10);
+    r->cap = mb << 20;
+    return r;
+  }();
+  return *c;
+}
+
+int cur_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+
+// frees every idle buffer and cached stream; returns how many buffers
+int cache_release_all() {
+  ResCache &c = res_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  int freed = 0;
+  const int dev0 = cur_device();
+  for (auto &kv : c.idle) {
+    (void)hipSetDevice(kv.first.first);
+    (void)hipFree(kv.second);
+    ++freed;
+  }
+  c.idle.clear();
+  c.idle_bytes = 0;
+  for (auto &st : c.streams) {
+    (void)hipSetDevice(st.device);
+    (void)hipEventDestroy(st.e0);
+    (void)hipEventDestroy(st.e1);
+    (void)hipStreamDestroy(st.s);
+  }
+  c.streams.clear();
+  (void)hipSetDevice(dev0);
+  return freed;
+}
+
 template <class T>
 void dfree(T *&p) {
-  if (p) (void)hipFree(p);
+  if (p) {
+    ResCache &c = res_cache();
+    {
+      std::lock_guard<std::mutex> lk(c.mu);
+      c.live.erase(static_cast<void *>(p));
+    }
+    (void)hipFree(p);
+  }
   p = nullptr;
+}
+
+// a buffer of a destroyed engine (its stream drained): into the cache while
+// it fits, else freed
+template <class T>
+void dretire(T *&p) {
+  if (!p) return;
+  ResCache &c = res_cache();
+  void *v = static_cast<void *>(p);
+  p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(v);
+    if (it != c.live.end() && c.idle_bytes + it->second <= c.cap) {
+      c.idle.emplace(std::make_pair(cur_device(), it->second), v);
+      c.idle_bytes += it->second;
+      c.live.erase(it);
+      return;
+    }
+    if (it != c.live.end()) c.live.erase(it);
+  }
+  (void)hipFree(v);
 }
 
 template <class T>
 int dalloc(T *&p, size_t count) {
   dfree(p);
   if (count == 0) return PBH_OK;
-  HIP_TRY(hipMalloc((void **)&p, count * sizeof(T)));
+  const size_t bytes = count * sizeof(T);
+  ResCache &c = res_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.idle.find(std::make_pair(cur_device(), bytes));
+    if (it != c.idle.end()) {
+      p = static_cast<T *>(it->second);
+      c.idle.erase(it);
+      c.idle_bytes -= bytes;
+      c.live.emplace(static_cast<void *>(p), bytes);
+      ++c.hits;
+      return PBH_OK;
+    }
+    ++c.misses;
+  }
+  hipError_t err = hipMalloc((void **)&p, bytes);
+  if (err == hipErrorOutOfMemory && cache_release_all() > 0) {
+    (void)hipGetLastError();
+    err = hipMalloc((void **)&p, bytes);
+  }
+  if (err != hipSuccess) {
+    p = nullptr;
+    return fail(PBH_ERR_HIP, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(err));
+  }
+  std::lock_guard<std::mutex> lk(c.mu);
+  c.live.emplace(static_cast<void *>(p), bytes);
   return PBH_OK;
 }
 
@@ -229,6 +350,15 @@ size_t pack(std::vector<double> &blk, const double *a, int64_t n) {
 
 int check_ptr(const void *p, const char *name) {
   return p ? PBH_OK : fail(PBH_ERR_ARG, "%s must not be NULL", name);
+}
+
+// init [n][d] (the caller's row-major chains) -> x [d][n]
+__global__ void chains_to_dim_major(const double *init, double *x, int64_t n, int32_t d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * d) {
+    const int64_t c = i / d, k = i - c * d;
+    x[k * n + c] = init[i];
+  }
 }
 
 __global__ void nacc_to_f64(const int64_t *nacc, double *out, int64_t n) {
@@ -542,13 +672,32 @@ int pbh_create(int device, pbh_engine **out) {
   // A/B switch for the markers' fences; default 0 = hipEventDefault)
   unsigned ev_flags = 0;
   if (const char *ef = std::getenv("PBH_EVENT_FLAGS")) ev_flags = (unsigned)std::strtoul(ef, nullptr, 0);
-  hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev0, ev_flags);
-  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev1, ev_flags);
+  e->ev_flags = ev_flags;
+  hipError_t err = hipSuccess;
+  {   // a destroyed engine's stream and events (drained), else new ones
+    ResCache &c = res_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (size_t i = 0; i < c.streams.size(); ++i)
+      if (c.streams[i].device == device && c.streams[i].flags == ev_flags) {
+        e->stream = c.streams[i].s;
+        e->ev0 = c.streams[i].e0;
+        e->ev1 = c.streams[i].e1;
+        c.streams.erase(c.streams.begin() + (ptrdiff_t)i);
+        break;
+      }
+  }
+  if (!e->stream) {
+    err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev0, ev_flags);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev1, ev_flags);
+  }
   if (err == hipSuccess) {
-    std::vector<double> tab(pbh::kBm64Doubles);
-    pbh::bm64_tables(tab.data());
-    err = hipMalloc((void **)&e->bm64, tab.size() * sizeof(double));
+    static const std::vector<double> tab = [] {   // computed once per process
+      std::vector<double> t(pbh::kBm64Doubles);
+      pbh::bm64_tables(t.data());
+      return t;
+    }();
+    if (dalloc(e->bm64, tab.size()) != PBH_OK) err = hipErrorOutOfMemory;
     if (err == hipSuccess)
       err = hipMemcpy(e->bm64, tab.data(), tab.size() * sizeof(double),
                       hipMemcpyHostToDevice);
@@ -566,25 +715,59 @@ int pbh_destroy(pbh_engine *e) {
   if (!e) return PBH_OK;
   (void)hipSetDevice(e->device);
   if (e->srv_active) (void)srv_stop(e);   // never leave the server running
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  bool drained = true;
+  if (e->stream) drained = hipStreamSynchronize(e->stream) == hipSuccess;
+  (void)hipGetLastError();
   if (e->comm) ncclCommDestroy(e->comm);
-  dfree(e->dmodel); dfree(e->dprop); dfree(e->dgibbs);
-  dfree(e->x); dfree(e->lp); dfree(e->rep); dfree(e->xo); dfree(e->gq); dfree(e->lx);
-  dfree(e->thr);
-  dfree(e->mt_key); dfree(e->mt_pos); dfree(e->mt_has); dfree(e->mt_order);
-  dfree(e->mt_gauss);
-  free_trace(e);
-  dfree(e->msum); dfree(e->msq); dfree(e->nacc);
-  dfree(e->gather_send); dfree(e->gather_recv); dfree(e->scalar);
-  dfree(e->bm64); dfree(e->ess); dfree(e->lgtab); dfree(e->ess_list); dfree(e->ess_tot);
+  // the device buffers into the resource cache (nothing in flight: the
+  // stream drained), or freed after a failed stream
+  auto put = [&](auto *&p) {
+    if (drained) dretire(p);
+    else dfree(p);
+  };
+  put(e->dmodel); put(e->dprop); put(e->dgibbs);
+  put(e->x); put(e->lp); put(e->rep); put(e->xo); put(e->gq); put(e->lx);
+  put(e->thr);
+  put(e->mt_key); put(e->mt_pos); put(e->mt_has); put(e->mt_order);
+  put(e->mt_gauss);
+  put(e->tx); put(e->tlp); put(e->tpx); put(e->tpp); put(e->ts); put(e->tacc);
+  e->cap = 0;
+  put(e->msum); put(e->msq); put(e->nacc);
+  put(e->gather_send); put(e->gather_recv); put(e->scalar);
+  put(e->bm64); put(e->ess); put(e->lgtab); dfree(e->ess_list); put(e->ess_tot);
   if (e->ess_host) (void)hipHostFree(e->ess_host);
   if (e->srv_cmd) (void)hipHostFree(e->srv_cmd);
   if (e->srv_done) (void)hipHostFree(e->srv_done);
   dfree(e->srv_mail);
-  if (e->ev0) (void)hipEventDestroy(e->ev0);
-  if (e->ev1) (void)hipEventDestroy(e->ev1);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  bool kept = false;
+  if (drained && e->stream && e->ev0 && e->ev1) {
+    ResCache &c = res_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.cap > 0 && c.streams.size() < 8) {
+      c.streams.push_back({e->device, e->ev_flags, e->stream, e->ev0, e->ev1});
+      kept = true;
+    }
+  }
+  if (!kept) {
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+  }
   delete e;
+  return PBH_OK;
+}
+
+int pbh_cache_release(void) {
+  (void)cache_release_all();
+  return PBH_OK;
+}
+
+int pbh_cache_info(int64_t *idle_bytes, int64_t *hits, int64_t *misses) {
+  ResCache &c = res_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (idle_bytes) *idle_bytes = (int64_t)c.idle_bytes;
+  if (hits) *hits = c.hits;
+  if (misses) *misses = c.misses;
   return PBH_OK;
 }
 
@@ -943,17 +1126,22 @@ int pbh_init_chains(pbh_engine *e, int64_t n, int64_t off, const double *init) {
   }
   // no ESS computed yet: every byte 0xFF is a NaN (all-ones exponent and
   // mantissa), set on the device instead of copying a host array of NaNs
-  HIP_TRY(hipMemset(e->ess, 0xFF, (size_t)d * n * sizeof(double)));
   e->gq_valid = false;
   e->lx_valid = false;
-  std::vector<double> xt((size_t)n * d);
-  for (int64_t c = 0; c < n; ++c)
-    for (int k = 0; k < d; ++k) xt[(size_t)k * n + c] = init[(size_t)c * d + k];
-  HIP_TRY(hipMemcpy(e->x, xt.data(), xt.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(e->lp, 0, n * sizeof(double)));
-  HIP_TRY(hipMemset(e->msum, 0, (size_t)n * d * sizeof(double)));
-  HIP_TRY(hipMemset(e->msq, 0, (size_t)n * d * sizeof(double)));
-  HIP_TRY(hipMemset(e->nacc, 0, n * sizeof(int64_t)));
+  hipStream_t st = e->stream;
+  const size_t nd = (size_t)n * d;
+  HIP_TRY(hipMemsetAsync(e->ess, 0xFF, nd * sizeof(double), st));
+  // the caller's [n][d] rows go up as they are (msum is the staging buffer,
+  // zeroed after) and are transposed to x's [d][n] on the device
+  HIP_TRY(hipMemcpyAsync(e->msum, init, nd * sizeof(double), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(chains_to_dim_major, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, st,
+                     e->msum, e->x, n, (int32_t)d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(e->lp, 0, n * sizeof(double), st));
+  HIP_TRY(hipMemsetAsync(e->msum, 0, nd * sizeof(double), st));
+  HIP_TRY(hipMemsetAsync(e->msq, 0, nd * sizeof(double), st));
+  HIP_TRY(hipMemsetAsync(e->nacc, 0, n * sizeof(int64_t), st));
+  HIP_TRY(hipStreamSynchronize(st));
   e->n = n;
   e->off = off;
   e->xo_seeded = false;
@@ -1202,6 +1390,9 @@ int pbh_get_replay(pbh_engine *e, int64_t first, int64_t n_steps, int32_t draw,
 // ---------------------------------------------------------------------------
 int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug) {
   if (check_ptr(e, "engine")) return PBH_ERR_ARG;
+  // PBH_TRACE_NOFILL: the caller's next run writes every record (no zero fill)
+  const bool nofill = (debug & PBH_TRACE_NOFILL) != 0;
+  debug &= ~PBH_TRACE_NOFILL;
   SRV_STOP(e);
   if (!e->x) return fail(PBH_ERR_STATE, "pbh_init_chains first");
   if (capacity < 0 || thin < 1) return fail(PBH_ERR_ARG, "bad capacity/thin");
@@ -1224,7 +1415,7 @@ int pbh_alloc_trace(pbh_engine *e, int64_t capacity, int32_t thin, int32_t debug
     free_trace(e);
     return rc;
   }
-  if (capacity > 0) {
+  if (capacity > 0 && !nofill) {
     // zero-fill: unwritten records read as zeros, and every page of the
     // trace is mapped and touched before the first run writes it (the
     // first writes of a short run otherwise pay the translation misses)

@@ -283,9 +283,12 @@ class Engine:
     return out
 
   # ---- running -----------------------------------------------------------
-  def alloc_trace(self, capacity, thin=1, debug=False):
+  def alloc_trace(self, capacity, thin=1, debug=False, fill=True):
+    """fill=False: no zero fill of the records (the next run writes every
+    one of them: PBH_TRACE_NOFILL)."""
+    flags = (1 if debug else 0) | (0 if fill else 0x100)
     _lib.call('pbh_alloc_trace', self._h, _c.c_int64(int(capacity)),
-              int(thin), 1 if debug else 0)
+              int(thin), flags)
     self.debug = bool(debug)
 
   def run(self, n_steps, steps_per_launch=0, sync=True):
@@ -591,6 +594,19 @@ class Engine:
     v = _c.c_double(float(value))
     _lib.call('pbh_rccl_allreduce_max', self._h, _c.byref(v))
     return v.value
+
+  @staticmethod
+  def cache_release():
+    """Frees the device buffers and streams destroyed engines left in the
+    library's resource cache (pbh_cache_release)."""
+    _lib.call('pbh_cache_release')
+
+  @staticmethod
+  def cache_info():
+    """(idle bytes, hits, misses) of the library's resource cache."""
+    v = [_c.c_int64() for _ in range(3)]
+    _lib.call('pbh_cache_info', *[_c.byref(x) for x in v])
+    return tuple(x.value for x in v)
 
   def close(self):
     if getattr(self, '_h', None) is not None and self._h.value:

@@ -1120,7 +1120,8 @@ class Sampler:
         # kernel, pbh_legacy_run); the thresholds stay on the device until a
         # step's t or the summary reads them
         self._drawn.append((self._g, k))   # steps drawn since seeding
-        eng.alloc_trace(k // self.thin, self.thin, debug=self.debug)
+        # (the run writes every record: no zero fill)
+        eng.alloc_trace(k // self.thin, self.thin, debug=self.debug, fill=False)
         eng.legacy_run(k, steps_per_launch=self.spl)
         if self.spec['proposal']['kind'] != 'gibbs':
           thin = self.thin
@@ -1130,7 +1131,7 @@ class Sampler:
         thr = thr.T[:, self.thin - 1::self.thin]
     elif self.rng == 'xoshiro':
       rewind['ck'] = eng.checkpoint()     # the generators at block start
-    eng.alloc_trace(k // self.thin, self.thin, debug=self.debug)
+    eng.alloc_trace(k // self.thin, self.thin, debug=self.debug, fill=False)
     eng.run(k, steps_per_launch=self.spl)
     return _DeviceTrace(eng, self.debug), thr, prev_x, prev_p
 
