@@ -60,6 +60,7 @@ struct pbh_engine {
   bool legacy_win = true;      // PBH_LEGACY_WIN=0: HBM-direct consumption (Mt2)
   bool legacy_fused = true;    // PBH_LEGACY_FUSED=0: pbh_legacy_run as generation + run
   bool legacy_wp = true;       // PBH_LEGACY_WP=0: the chain-per-lane generator for MH streams
+  bool legacy_ahead = true;    // PBH_LEGACY_AHEAD=0: no twist-ahead pass before fused launches
   bool mt_odd = false;         // a stream may sit at an odd word (randint drew single words)
   bool rec_thr = false;        // pbh_set_record_threshold: keep pbh_legacy_run's thresholds
   double *thr = nullptr;       // [thr_steps][n] thresholds of the last pbh_legacy_run
@@ -172,7 +173,9 @@ struct pbh_engine {
 namespace {
 
 // words of legacy state per chain in each layout (pbh_engine.mt_mode)
-int64_t mt_words(int mode) { return mode == 2 ? 4 * 20 * 32 : mode == 1 ? 2 * 624 : 624; }
+constexpr double pbh_mt_block_words() { return 624.0; }
+// (mode 2: pbh_mt.h kK4 = 16 buffers of 20 chunks of 32 words)
+int64_t mt_words(int mode) { return mode == 2 ? 16 * 20 * 32 : mode == 1 ? 2 * 624 : 624; }
 
 thread_local std::string g_err;
 
@@ -668,6 +671,7 @@ int pbh_create(int device, pbh_engine **out) {
   if (const char *lk = std::getenv("PBH_LEGACY_K4")) e->legacy_k4 = std::atoi(lk) != 0;
   if (const char *lf = std::getenv("PBH_LEGACY_FUSED")) e->legacy_fused = std::atoi(lf) != 0;
   if (const char *lp = std::getenv("PBH_LEGACY_WP")) e->legacy_wp = std::atoi(lp) != 0;
+  if (const char *la = std::getenv("PBH_LEGACY_AHEAD")) e->legacy_ahead = std::atoi(la) != 0;
   // PBH_EVENT_FLAGS: hipEventCreateWithFlags flags of the timing events (an
   // A/B switch for the markers' fences; default 0 = hipEventDefault)
   unsigned ev_flags = 0;
@@ -1777,9 +1781,39 @@ int pbh_legacy_run(pbh_engine *e, int64_t n_steps, int32_t steps_per_launch) {
   }
   // launches of at most 2^20 steps, as pbh_legacy_replay (Mt4's 32-bit head)
   constexpr int64_t kLegacyLaunchSteps = int64_t(1) << 20;
+  // twist-ahead (legacy_ahead_kernel, PBH_LEGACY_AHEAD=0 off): each launch's
+  // blocks are twisted before it by one wavefront per chain, so the fused
+  // kernel only consumes; a launch is at most what 15 blocks ahead hold with
+  // an 8-sigma margin on the polar method's attempts (a chain that needs more
+  // twists in the fused kernel, as without the pre-pass)
+  const bool ahead = e->legacy_ahead && e->mt_mode == 2 && !e->mt_odd;
+  const double dd = (double)e->d;
+  // doubles per step (mean, variance): normal -- d/2 pairs at 4/pi attempts
+  // of two doubles (attempt-count variance 0.348 per pair) + the threshold;
+  // raw -- d + 1
+  const double dmean = la.normal ? 4.0 * dd / 3.14159265358979 + 1.0 : dd + 1.0;
+  const double dvar = la.normal ? 4.0 * 0.3480 * dd / 2.0 : 0.0;
+  auto ahead_words = [&](int64_t m) {   // words of m steps, 8 sigma
+    return 2.0 * ((double)m * dmean + 8.0 * std::sqrt((double)m * dvar) + 2.0);
+  };
+  int64_t m_fit = spl;
+  if (ahead) {   // 14 whole blocks after the current one's (up to 624) words
+    while (m_fit > 1 && ahead_words(m_fit) > 14.0 * pbh_mt_block_words()) m_fit = m_fit * 7 / 8;
+  }
   int64_t launches = 0;
   for (int64_t done = 0; done < n_steps;) {
-    const int64_t m = std::min(std::min(spl, kLegacyLaunchSteps), n_steps - done);
+    int64_t m = std::min(std::min(spl, kLegacyLaunchSteps), n_steps - done);
+    if (ahead) {
+      m = std::min(m, m_fit);
+      const int32_t want = std::min<int32_t>(
+          15, 1 + (int32_t)std::ceil(ahead_words(m) / pbh_mt_block_words()));
+      const hipError_t ea = pbh::launch_legacy_ahead(e->mt_key, e->mt_pos, e->n, want,
+                                                     e->stream);
+      if (ea != hipSuccess) {
+        lev = {};
+        return fail(PBH_ERR_HIP, "pbh_legacy_run (twist-ahead): %s", hipGetErrorString(ea));
+      }
+    }
     if (!e->event_markers && done + m >= n_steps) lev.stop = e->ev1;
     k.n_steps = (int32_t)m;
     k.g0 = e->g;

@@ -257,6 +257,10 @@ hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,
                               int64_t n, int32_t db, hipStream_t s);
 hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s);
+// Mt4 state: twist every chain's buffers ahead until `want` (<= 15) blocks
+// follow its current one (legacy_ahead_kernel)
+hipError_t launch_legacy_ahead(uint32_t *key, int32_t *pos, int64_t n, int32_t want,
+                               hipStream_t s);
 // The fused REPLAY kernel: generation and the REPLAY chain-step in one
 // launch (la: the generator's state, a: the run's kernel arguments, a.n_steps
 // = la.n_steps).  hipErrorNotSupported: the form is not covered (the caller

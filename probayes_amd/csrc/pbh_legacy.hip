@@ -620,7 +620,7 @@ struct Mt3 {
 // block of 156 quads padded to 160, and a chunk is one 128-byte line per lane,
 // so the window's refills (whole chunks) and the twists move whole lines
 // whatever the other lanes' positions.
-// Packed state: pos | cb << 16 | ready << 18 (cb = the current block's buffer).
+// Packed state: pos | cb << 16 | ready << 20 (4-bit fields: kK4 = 16 buffers) (cb = the current block's buffer).
 // ---------------------------------------------------------------------------
 // The twist through a raw buffer resource over the whole state (the engine
 // takes this layout only while it spans < 2^32 bytes): each lane's source and
@@ -703,10 +703,10 @@ __device__ __attribute__((noinline)) uint64_t mt4_refill_cold(w4 *key, int64_t n
   for (int k = 0; k < NC; ++k) {
     const int hb = hq / kQ, hc = (hq - hb * kQ) >> 3;
     if (hb - blk > ready) {   // the head's block is not twisted yet
-      mt4_twist_cold(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
+      mt4_twist_cold(key, n, c, (cb + ready) & kBufMask, (cb + ready + 1) & kBufMask);
       ++ready;
     }
-    hq += mt4_stage<DBL>(key, n, c, win, 2 * H, (cb + hb - blk) & 3, hc, hq);
+    hq += mt4_stage<DBL>(key, n, c, win, 2 * H, (cb + hb - blk) & kBufMask, hc, hq);
   }
   return ((uint64_t)(uint32_t)ready << 32) | (uint32_t)hq;
 }
@@ -770,7 +770,7 @@ struct Mt4 {
     int b = hb, ch = hc;
 #pragma unroll
     for (int k = 0; k < kRC; ++k) {
-      mt4_load(key, n, c, (cb + b - blk) & 3, ch, pfv[k]);
+      mt4_load(key, n, c, (cb + b - blk) & kBufMask, ch, pfv[k]);
       if (++ch == kCh) {
         ch = 0;
         ++b;
@@ -792,8 +792,8 @@ struct Mt4 {
 
   __device__ __forceinline__ void init(int st, w4 *w) {
     pos = st & 0xFFFF;
-    cb = (st >> 16) & 3;
-    ready = (st >> 18) & 3;
+    cb = (st >> 16) & kBufMask;
+    ready = (st >> 20) & kBufMask;
     blk = 0;
     win = w;
     hb = 0;
@@ -810,7 +810,7 @@ struct Mt4 {
     const bool due = ready == 0 && (pos >= kRefill || hb > blk || hc + kRC > kCh);
     if (__builtin_amdgcn_ballot_w64(due)) {
       if (ready < kK4 - 1) {   // every lane with a free buffer: one block further
-        mt4_twist(key, n, c, (cb + ready) & 3, (cb + ready + 1) & 3);
+        mt4_twist(key, n, c, (cb + ready) & kBufMask, (cb + ready + 1) & kBufMask);
         ++ready;
       }
     }
@@ -833,10 +833,10 @@ struct Mt4 {
 
   __device__ __forceinline__ void flip() {   // into the next block (pos = kN)
     if (ready == 0) {   // nothing twisted ahead (a step longer than half a block)
-      mt4_twist_cold(key, n, c, cb, (cb + 1) & 3);
+      mt4_twist_cold(key, n, c, cb, (cb + 1) & kBufMask);
       ready = 1;
     }
-    cb = (cb + 1) & 3;
+    cb = (cb + 1) & kBufMask;
     --ready;
     pos = 0;
     ++blk;
@@ -953,7 +953,7 @@ struct Mt4 {
       if (pos & 3) cur = slot(aq());
   }
 
-  __device__ __forceinline__ int packed() const { return pos | (cb << 16) | (ready << 18); }
+  __device__ __forceinline__ int packed() const { return pos | (cb << 16) | (ready << 20); }
 };
 
 // Seeding for Mt4: init_genrand into buffer 0, the first twist into buffer 1;
@@ -974,7 +974,7 @@ __global__ __launch_bounds__(256) void mt_seed_k4_kernel(uint32_t *key, int32_t 
     k4q(qk, n, c, 0, i) = w;
   }
   mt4_twist(qk, n, c, 0, 1);
-  pos[c] = 0 | (1 << 16) | (0 << 18);
+  pos[c] = 0 | (1 << 16) | (0 << 20);
   gauss[c] = 0.0;
   has_gauss[c] = 0;
 }
@@ -1520,6 +1520,60 @@ struct LegacyDraws {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Timing-only probe (PBH_LEGACY_FAKE=1; wrong streams, never a result): the
+// fused kernel with the Mt4 generator replaced by a counter hash of the same
+// interface -- no state in HBM, no twist, no window -- so that its time is
+// what the polar method, the REPLAY step and the trace cost without MT19937.
+// ---------------------------------------------------------------------------
+struct FakeM {
+  static constexpr bool kLockstep = true, kPeek = true, kPeek4 = true, kLogTab = true;
+  uint32_t ctr, key;
+  __device__ __forceinline__ static uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+  }
+  __device__ __forceinline__ double dbl(uint32_t i) const {
+    const uint32_t a = mix(i ^ key), b = mix(i + 0x9E3779B9u * key);
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+  }
+  __device__ __forceinline__ void maintain() {}
+  __device__ __forceinline__ double next_double() { return dbl(ctr++); }
+  __device__ __forceinline__ void attempts4(double (&x1)[4], double (&x2)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x1[i] = 2.0 * dbl(ctr + 2 * i) - 1.0;
+      x2[i] = 2.0 * dbl(ctr + 2 * i + 1) - 1.0;
+    }
+  }
+  __device__ __forceinline__ void advance(int nw) { ctr += (uint32_t)nw / 2; }
+};
+
+template <int D, bool NORMAL, int TGT, int PROP>
+__global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void legacy_mh_fake_kernel(LegacyArgs la, KArgs a) {
+  extern __shared__ w4 s_lw[];
+  __shared__ double s_lg[kLegLogDoubles];
+  for (int i = threadIdx.x; i < kLegLogDoubles; i += kBlockLegacy) s_lg[i] = la.lgtab[i];
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * kBlockLegacy + threadIdx.x;
+  if (c >= la.n) return;
+  FakeM m{(uint32_t)la.step0 * 64u, (uint32_t)c * 0x85ebca6bu + 1u};
+  LegacyDraws<FakeM, NORMAL> src{m, reinterpret_cast<double2 *>(s_lw), s_lg,
+                                 la.gauss[c], la.has_gauss[c], la.thr, la.n};
+  mh_body<D, PBH_RNG_REPLAY, TGT, PROP>(a, src, nullptr, false);
+  la.gauss[c] = src.gauss;
+  la.has_gauss[c] = src.has;
+}
+
+bool legacy_fake_on() {
+  static const bool on = [] {
+    const char *p = std::getenv("PBH_LEGACY_FAKE");
+    return p && p[0] == '1';
+  }();
+  return on;
+}
+
 template <int D, int H, bool NORMAL, int TGT, int PROP>
 __global__ __launch_bounds__(kBlockLegacy) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void legacy_mh_kernel(LegacyArgs la, KArgs a) {
@@ -1566,6 +1620,16 @@ hipError_t launch_legacy_mh_t(const LegacyArgs &la, const KArgs &a, hipStream_t 
 template <int D>
 hipError_t launch_legacy_mh_d(const LegacyArgs &la, const KArgs &a, hipStream_t s) {
   constexpr int H = D <= 12 ? 16 : 8;   // the window while the stage leaves room
+  if constexpr (D == 10) {
+    if (legacy_fake_on() && la.normal && a.target == PBH_TARGET_DIAG_GAUSS &&
+        a.prop == PBH_PROP_GAUSS) {   // timing-only probe (see FakeM)
+      constexpr size_t lds = (size_t)((D + 1) / 2) * kBlockLegacy * sizeof(uint4);
+      const dim3 grid((unsigned)((la.n + kBlockLegacy - 1) / kBlockLegacy)), block(kBlockLegacy);
+      hipLaunchKernelGGL((legacy_mh_fake_kernel<D, true, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>),
+                         grid, block, lds, s, la, a);
+      return hipGetLastError();
+    }
+  }
   if (la.normal) {
     if (a.target == PBH_TARGET_DIAG_GAUSS && a.prop == PBH_PROP_GAUSS)   // cfg2's form
       return launch_legacy_mh_t<D, H, true, PBH_TARGET_DIAG_GAUSS, PBH_PROP_GAUSS>(la, a, s);
@@ -1576,7 +1640,71 @@ hipError_t launch_legacy_mh_d(const LegacyArgs &la, const KArgs &a, hipStream_t 
 
 
 
+// ---------------------------------------------------------------------------
+// Twist-ahead (legacy_ahead_kernel, round 6): before a fused REPLAY launch,
+// every chain's Mt4 buffers after its current block are twisted in advance
+// (`ready` raised to the launch's need), so that the fused kernel -- one
+// chain per lane, one wavefront per SIMD at 65 536 chains, latency-bound --
+// only consumes (window refills: load, temper, convert) and never twists in
+// its own step loop.  Here ONE WAVEFRONT twists ONE chain's blocks: the block
+// sits in LDS (624 words), the 64 lanes twist it in five 128-word iterations
+// (the sequential twist's three ranges are whole iterations apart: words i <
+// 227 read the old words i + 397, the rest the new words i - 227, and word
+// 623 the new word 0), and each new block is stored to its buffer as whole
+// 128-byte lines.  The buffers' contents and the packed state are exactly
+// what the fused kernel's own twist rounds would have left (the twist is a
+// pure function of the previous block), so streams are unchanged.
+// ---------------------------------------------------------------------------
+constexpr int kAheadW = 4;   // chains (wavefronts) per workgroup
+
+__global__ __launch_bounds__(64 * kAheadW) void legacy_ahead_kernel(uint32_t *key_, int32_t *pos,
+                                                                     int64_t n, int32_t want) {
+  __shared__ uint32_t sh[kAheadW][kN];
+  const int lane = threadIdx.x & 63;
+  uint32_t *const mt = sh[threadIdx.x >> 6];
+  const int64_t c = (int64_t)blockIdx.x * kAheadW + (threadIdx.x >> 6);
+  if (c >= n) return;   // the whole wave
+  w4 *const key = reinterpret_cast<w4 *>(key_);
+  const int st = pos[c];
+  const int cb = (st >> 16) & kBufMask, ready = (st >> 20) & kBufMask;
+  if (ready >= want) return;   // wave-uniform
+  // the last twisted block (current + ready) into LDS
+  const int src = (cb + ready) & kBufMask;
+  for (int i = lane; i < kQ; i += 64)
+    *reinterpret_cast<w4 *>(&mt[4 * i]) = k4q(key, n, c, src, i);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  for (int r = ready; r < want; ++r) {
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {
+      const int k = lane + 64 * it;
+      if (k < kN / 2) {
+        const int i0 = 2 * k;
+        const uint2 o = *reinterpret_cast<const uint2 *>(&mt[i0]);
+        const uint32_t o2 = mt[i0 + 2 < kN ? i0 + 2 : 0];
+        const uint32_t f0 = mt[i0 < kN - kM ? i0 + kM : i0 - (kN - kM)];
+        const uint32_t f1 = mt[i0 + 1 < kN - kM ? i0 + 1 + kM : i0 + 1 - (kN - kM)];
+        *reinterpret_cast<uint2 *>(&mt[i0]) = make_uint2(f0 ^ mt_f(o.x, o.y), f1 ^ mt_f(o.y, o2));
+      }
+      // this iteration's words before the next one's reads (one wavefront:
+      // its LDS operations complete in order)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    const int dst = (cb + r + 1) & kBufMask;
+    for (int i = lane; i < kQ; i += 64)
+      k4q(key, n, c, dst, i) = *reinterpret_cast<const w4 *>(&mt[4 * i]);
+  }
+  if (lane == 0) pos[c] = (st & 0xFFFF) | (cb << 16) | (want << 20);
+}
+
 }  // namespace
+
+hipError_t launch_legacy_ahead(uint32_t *key, int32_t *pos, int64_t n, int32_t want,
+                               hipStream_t s) {
+  if (want < 1 || want > kK4 - 1) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((n + kAheadW - 1) / kAheadW)), block(64 * kAheadW);
+  hipLaunchKernelGGL(legacy_ahead_kernel, grid, block, 0, s, key, pos, n, want);
+  return hipGetLastError();
+}
 
 hipError_t launch_legacy_seed(uint32_t *key, int32_t *pos, double *gauss,
                               int32_t *has_gauss, const uint32_t *seeds,

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64 * kWpW) void legacy_gen_wp_kernel(LegacyArgs a) 
   double *const out = a.out + c;
   // the chain's state: the current block from buffer cb (Mt4's layout)
   const int st = a.pos[c];
-  const int pos0 = st & 0xFFFF, cb = (st >> 16) & 3;
+  const int pos0 = st & 0xFFFF, cb = (st >> 16) & kBufMask;
   w4 *const key = reinterpret_cast<w4 *>(a.key);
   for (int i = lane; i < kQ; i += 64)
     *reinterpret_cast<w4 *>(&W.mt[4 * i]) = k4q(key, n, c, cb, i);

@@ -18,7 +18,11 @@ __device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b) {
   return (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
 }
 typedef uint32_t w4 __attribute__((ext_vector_type(4)));
-constexpr int kK4 = 4, kCh = 20;   // buffers; 8-quad chunks per (padded) block
+// Mt4's buffers per chain (a power of two: the current block and up to
+// kK4 - 1 twisted ahead; legacy_ahead_kernel fills them before a fused
+// REPLAY launch) and 8-quad chunks per (padded) block
+constexpr int kK4 = 16, kCh = 20;
+constexpr int kBufMask = kK4 - 1;
 __device__ __forceinline__ w4 &k4q(w4 *key, int64_t n, int64_t c, int b, int i) {
   return key[((int64_t)(b * kCh + (i >> 3)) * n + c) * 8 + (i & 7)];
 }
