@@ -12,3 +12,5 @@ for a in 1 0; do
 timeout -k 10 120 env PBH_LEGACY_AHEAD=$a python scripts/replay_fused_probe.py 65536 1000 250 fused >> $OUT/ahead$a.jsonl 2>&1 || exit $?
 done
 done
+R=$PWD
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $R/scripts/replay_fused_probe.py 65536 1000 250 fused > $R/$OUT/trace.log 2>&1 || exit $?
