@@ -623,8 +623,8 @@ class SP:
     if self._counter is None:
       self.reset()
     step = sampler._next_step()
-    self._counter[sampler] += sampler.thin
-    self._last[sampler] = step   # OPQR(None, step.v, None, None) when read
+    self._counter.add(sampler, sampler.thin)
+    self._last.put(sampler, step)   # OPQR(None, step.v, None, None) when read
     return step
 
   # ---- sampling (sp.py:261-295) ---------------------------------------------
@@ -656,6 +656,19 @@ class SP:
       warnings.warn(
           "No stop specification set - this walk may proceed indefinitely")
     steps = collections.deque()
+    if stop is None and isinstance(sampler, Sampler):
+      # nothing runs between the steps of this loop: the rest of each
+      # computed block is handed out at once (the same Steps, counters, last
+      # state and hand-out position as one next() per step)
+      while True:
+        bulk = sampler._bulk_steps()
+        if bulk:
+          steps.extend(bulk)
+          continue
+        try:
+          steps.append(next(sampler))
+        except StopIteration:
+          return steps
     for sample in sampler:
       if stop is not None and len(steps) >= stop:
         break
@@ -699,6 +712,14 @@ class _LastStates(weakref.WeakKeyDictionary):
   def get(self, key, default=None):
     return self[key] if key in self else default
 
+  def put(self, key, v):
+    """self[key] = v through a registered sampler's own weak reference."""
+    r = getattr(key, '_ref', None)
+    if r is not None and r in self.data:
+      self.data[r] = v
+    else:
+      self[key] = v
+
   def values(self):
     return [self[k] for k in list(self.keys())]
 
@@ -713,7 +734,17 @@ class _WeakCounter(weakref.WeakKeyDictionary):
   device buffers.  Missing samplers count 0, as in a Counter."""
 
   def __getitem__(self, key):
-    return self.data.get(weakref.ref(key), 0)
+    r = getattr(key, '_ref', None)
+    return self.data.get(r if r is not None else weakref.ref(key), 0)
+
+  def add(self, key, k):
+    """counter[key] += k; a registered sampler's own weak reference finds
+    its entry (no new weakref per step: ~0.3 us of each handed-out step)."""
+    r = getattr(key, '_ref', None)
+    if r is not None and r in self.data:
+      self.data[r] += k
+    else:
+      self[key] = self[key] + k
 
 
 OPQRSTUV = collections.namedtuple('opqrstuv', ['o', 'p', 'q', 'r', 's', 't',
@@ -927,6 +958,8 @@ class Sampler:
     self._ahead = self.chunk
     self.n_computed = 0     # chain-steps' worth of steps run (diagnostic)
     self._prev = None       # the state before the next block, when known on the host
+    self._ref = weakref.ref(self)   # the SP registry's key for this sampler
+    self._gibbs = None      # _is_gibbs(), fixed once lowered
 
   def __repr__(self):
     return '<probayes_amd Sampler {} stop={}>'.format(self.sid, self.stop)
@@ -947,15 +980,43 @@ class Sampler:
       raise StopIteration
     return self.sp.next(self)
 
+  def _bulk_steps(self):
+    """The steps next() would hand out from the current block, all at once,
+    when no per-step work is due (not after the block's end or the stop, no
+    global-stream rewind states, no Gibbs cycle phase): SP.walk's fast path.
+    Returns [] when the next step needs next()."""
+    cur = self._cur
+    if (self._done or self._epoch or cur is None or self._gibbs is not False or
+        'states' in cur.rewind or self._j >= cur.T):
+      return []
+    k = cur.T - self._j
+    if self.stop is not None:
+      k = min(k, (self.stop - self.sp.get_counter(self)) // self.thin)
+    if k <= 0:
+      return []
+    j0 = self._j
+    out = [Step(self, cur, j) for j in range(j0, j0 + k)]
+    self._j = j0 + k
+    self._handed = (cur, j0 + k - 1)
+    self.sp._counter.add(self, k * self.thin)
+    self.sp._last.put(self, out[-1])
+    return out
+
   # ---- set-up ------------------------------------------------------------
   def _init_array(self):
     d, n = len(self.names), self.n
     init = {_key(k): v for k, v in (self.init or {}).items()}
     out = np.empty((n, d))
-    for i, k in enumerate(self.names):
+    vals = []
+    for k in self.names:
       if k not in init:
         raise ValueError('init value missing for {}'.format(k))
-      out[:, i] = np.broadcast_to(np.asarray(init[k], np.float64), (n,))
+      vals.append(np.asarray(init[k], np.float64))
+    if all(v.size == 1 for v in vals):   # one row for every chain: a contiguous fill
+      out[:] = np.array([float(v.reshape(-1)[0]) for v in vals])
+      return out
+    for i, v in enumerate(vals):
+      out[:, i] = np.broadcast_to(v, (n,))
     return out
 
   def _is_gibbs(self):
@@ -982,6 +1043,7 @@ class Sampler:
       return
     self.spec = self.sp.lower(self.extra, self.iid, self.joint)
     self.pscale = self.spec['pscale']
+    self._gibbs = self._is_gibbs()
     if self.rng == 'legacy' and self.batched and self.seeds is None:
       raise ValueError("rng='legacy' with chains=N needs seeds=[...]")
     if self.spec.get('kind') == 'linreg' and self.thin != 1:
@@ -1230,7 +1292,7 @@ class Sampler:
       if self._j >= cur.T:   # fully handed out: no rewind into it any more
         del cur.rewind['states']
     self._handed = (cur, j)
-    if self._is_gibbs():   # the RF's __cond_mod follows the steps handed out
+    if self._gibbs:   # the RF's __cond_mod follows the steps handed out
       self._cycle_rf()._pbh_cond_step = \
           (cur.g0 + (j + 1) * self.thin) % self._cycle_len()
     return Step(self, cur, j)

@@ -9,7 +9,7 @@ summary.  One JSON line per repetition:
                 objects; the trace stays on the device;
   summary_s  -- SP(samples): the trace copied to the host and the PDs built;
   chain_steps_per_s -- N T / walk_s, beside bench.py's replay_chain_steps_per_s.
-usage: facade_workload.py [chains] [steps] [reps] [steps_per_launch]"""
+usage: facade_workload.py [chains] [steps] [reps] [steps_per_launch] [walk|iter]"""
 import json
 import os
 import sys
@@ -27,6 +27,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 spl = int(sys.argv[4]) if len(sys.argv) > 4 else 250   # bench.py's REPLAY launches
+walk = (sys.argv[5] if len(sys.argv) > 5 else 'walk') == 'walk'   # or 'iter': next() per step
 builder, params, _, _, _ = WORKLOADS['diag10']
 process, init, extra, kwds, keys = builder(pb, params)
 args = (init,) if extra is None else (init, extra)
@@ -35,19 +36,25 @@ for rep in range(reps + 1):   # the first is a warm-up (library load, allocation
   t0 = time.perf_counter()
   sm = process.sampler(*args, stop=T, chains=n, seeds=seeds,
                        steps_per_launch=spl, **kwds)
-  it = iter(sm)
-  first = next(it)            # the engine run: all T steps
-  tf = time.perf_counter()
-  samples = [first] + list(it)
-  t1 = time.perf_counter()
+  if walk:   # SP.walk, as examples/mcmc consume a sampler
+    samples = process.walk(sm)
+    tf = t1 = time.perf_counter()
+  else:
+    it = iter(sm)
+    first = next(it)            # the engine run: all T steps
+    tf = time.perf_counter()
+    samples = [first] + list(it)
+    t1 = time.perf_counter()
   summary = process(samples)
   t2 = time.perf_counter()
   assert np.asarray(summary.v[keys[0]]).shape == (T, n)
   sm.close()
   if rep:
     print(json.dumps({'workload': 'facade seeded diag10 (cfg2 shape)', 'chains': n,
+                      'consumed_by': 'SP.walk' if walk else 'next() per step',
                       'steps': T, 'steps_per_launch': spl, 'walk_s': t1 - t0,
-                      'first_step_s': tf - t0, 'other_steps_s': t1 - tf,
+                      'first_step_s': None if walk else tf - t0,
+                      'other_steps_s': None if walk else t1 - tf,
                       'summary_s': t2 - t1,
                       'chain_steps_per_s': n * T / (t1 - t0),
                       'end_to_end_chain_steps_per_s': n * T / (t2 - t0)}), flush=True)
