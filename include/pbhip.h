@@ -223,9 +223,10 @@ int pbh_restore(pbh_engine *eng, const double *x, const double *lp,
                 int64_t step, int32_t has_pred, const uint32_t *xo);
 /* The device legacy streams' state for a checkpoint (pbh_legacy_seed):
  * key [words][N] with words per chain from pbh_legacy_state_words (624 in
- * place, 1248 double-buffered, 2560 for the default four-block chunked
- * layout; the words are the device layout, opaque to the caller and valid
- * only for an engine seeded with the same layout), the read position pos [N]
+ * place, 1248 double-buffered, 640 for the default chunked layout: the
+ * current block, moved into buffer 0 by the get; the words are the device
+ * layout, opaque to the caller and valid only for an engine seeded with the
+ * same layout), the read position pos [N]
  * (packed with the layout's buffer indices), the cached-gauss flag
  * has [N] and value gauss [N] (NumPy's RandomState has_gauss / gauss).
  * After pbh_restore on an engine with legacy streams, pbh_legacy_replay

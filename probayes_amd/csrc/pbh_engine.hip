@@ -176,6 +176,9 @@ namespace {
 constexpr double pbh_mt_block_words() { return 624.0; }
 // (mode 2: pbh_mt.h kK4 = 16 buffers of 20 chunks of 32 words)
 int64_t mt_words(int mode) { return mode == 2 ? 16 * 20 * 32 : mode == 1 ? 2 * 624 : 624; }
+// words per chain of the checkpoint form (pbh_get/set_legacy_state): Mt4's
+// current block alone, moved into buffer 0 (launch_legacy_normalize)
+int64_t mt_state_words(int mode) { return mode == 2 ? 20 * 32 : mt_words(mode); }
 
 thread_local std::string g_err;
 
@@ -2163,7 +2166,7 @@ int pbh_set_chain_logs(pbh_engine *e, const double *lx) {
 
 int pbh_legacy_state_words(pbh_engine *e, int64_t *words) {
   if (check_ptr(e, "engine") || check_ptr(words, "words")) return PBH_ERR_ARG;
-  *words = e->mt_key ? mt_words(e->mt_mode) : 0;
+  *words = e->mt_key ? mt_state_words(e->mt_mode) : 0;
   return PBH_OK;
 }
 
@@ -2176,8 +2179,10 @@ int pbh_get_legacy_state(pbh_engine *e, uint32_t *key, int32_t *pos,
   if (!e->mt_key) return fail(PBH_ERR_STATE, "no legacy streams (pbh_legacy_seed)");
   if (e->mt_stale) return fail(PBH_ERR_STATE, "legacy state stale after pbh_restore");
   const int64_t n = e->n;
-  const size_t kw = (size_t)mt_words(e->mt_mode) * n;
+  const size_t kw = (size_t)mt_state_words(e->mt_mode) * n;
   HIP_TRY(hipSetDevice(e->device));
+  if (e->mt_mode == 2)   // the current blocks into buffer 0: the key's prefix
+    HIP_TRY(pbh::launch_legacy_normalize(e->mt_key, e->mt_pos, n, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(key, e->mt_key, kw * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(pos, e->mt_pos, n * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -2194,11 +2199,17 @@ int pbh_set_legacy_state(pbh_engine *e, const uint32_t *key, const int32_t *pos,
   SRV_STOP(e);
   if (!e->mt_key) return fail(PBH_ERR_STATE, "pbh_legacy_seed first (the layout)");
   const int64_t n = e->n;
-  const size_t kw = (size_t)mt_words(e->mt_mode) * n;
+  const size_t kw = (size_t)mt_state_words(e->mt_mode) * n;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(e->mt_key, key, kw * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->mt_pos, pos, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (e->mt_mode == 2) {   // the checkpoint form: the block in buffer 0
+    std::vector<int32_t> p0(pos, pos + n);
+    for (auto &v : p0) v &= 0xFFFF;
+    HIP_TRY(hipMemcpy(e->mt_pos, p0.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  } else {
+    HIP_TRY(hipMemcpy(e->mt_pos, pos, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy(e->mt_has, has, n * sizeof(int32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->mt_gauss, gauss, n * sizeof(double), hipMemcpyHostToDevice));
   e->mt_stale = false;

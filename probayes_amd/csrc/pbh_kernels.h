@@ -261,6 +261,9 @@ hipError_t launch_legacy_gen(const LegacyArgs &a, hipStream_t s);
 // follow its current one (legacy_ahead_kernel)
 hipError_t launch_legacy_ahead(uint32_t *key, int32_t *pos, int64_t n, int32_t want,
                                hipStream_t s);
+// Mt4 state: each chain's current block into buffer 0, buffer / ready fields
+// of pos cleared (the checkpoint form: the first 20 x 32 words per chain)
+hipError_t launch_legacy_normalize(uint32_t *key, int32_t *pos, int64_t n, hipStream_t s);
 // The fused REPLAY kernel: generation and the REPLAY chain-step in one
 // launch (la: the generator's state, a: the run's kernel arguments, a.n_steps
 // = la.n_steps).  hipErrorNotSupported: the form is not covered (the caller

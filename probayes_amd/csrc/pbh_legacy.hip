@@ -1696,7 +1696,35 @@ __global__ __launch_bounds__(64 * kAheadW) void legacy_ahead_kernel(uint32_t *ke
   if (lane == 0) pos[c] = (st & 0xFFFF) | (cb << 16) | (want << 20);
 }
 
+// The checkpoint form of the Mt4 state: every chain's current block moved
+// into buffer 0 (quad per thread) and its packed position's buffer and
+// ready fields cleared (the blocks twisted ahead are dropped: the next run
+// twists them again, the same words), so that the state is the prefix of
+// 20 chunks x 32 words per chain of the key array
+__global__ __launch_bounds__(256) void legacy_norm_copy_kernel(w4 *key, const int32_t *pos,
+                                                              int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * kCh * 8) return;
+  const int64_t c = t / (kCh * 8);
+  const int i = (int)(t - c * (kCh * 8));
+  const int cb = (pos[c] >> 16) & kBufMask;
+  if (cb != 0) k4q(key, n, c, 0, i) = k4q(key, n, c, cb, i);
+}
+__global__ __launch_bounds__(256) void legacy_norm_pos_kernel(int32_t *pos, int64_t n) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n) pos[c] &= 0xFFFF;
+}
+
 }  // namespace
+
+hipError_t launch_legacy_normalize(uint32_t *key, int32_t *pos, int64_t n, hipStream_t s) {
+  const int64_t q = n * kCh * 8;
+  hipLaunchKernelGGL(legacy_norm_copy_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<w4 *>(key), pos, n);
+  hipLaunchKernelGGL(legacy_norm_pos_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     pos, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_legacy_ahead(uint32_t *key, int32_t *pos, int64_t n, int32_t want,
                                hipStream_t s) {

@@ -441,7 +441,7 @@ class Engine:
       _lib.call('pbh_legacy_state_words', self._h, _c.byref(words))
       want = {'key': (words.value, self.n), 'pos': (self.n,), 'has': (self.n,),
               'gauss': (self.n,)}
-      layouts = {10240: 'Mt4, sixteen chunked blocks (the default since round 6)',
+      layouts = {640: 'Mt4, its current chunked block (the default since round 6)',
                  2560: 'Mt4, four chunked blocks (rounds 4-5)',
                  1248: 'double-buffered window (PBH_LEGACY_K4=0, round 3)',
                  624: 'in-place state (PBH_LEGACY_DB=0, round 1)'}
