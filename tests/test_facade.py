@@ -338,3 +338,68 @@ def test_summary_o_q_r_match_reference(name):
       assert _golden_rtol(np.ravel(d[k]), ref) <= 1e-12, (f, k)
     ref = g['{}/{}/prob'.format(name, f)]
     assert _golden_rtol(np.ravel(d.prob), ref) <= 1e-12, (f, 'prob')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['diag10', 'gibbs8', 'metrohast_norm1d'])
+@pytest.mark.parametrize('stop', [None, 7])
+def test_walk_hands_out_what_next_does(name, stop):
+  """SP.walk's bulk hand-out (Sampler._bulk_steps) against one next() per
+  step on a twin sampler: the same records, counters and last state, for a
+  bounded sampler walked whole and cut at a stop, with thin > 1, and the
+  sampler continuing after the walk."""
+  builder, params, n, t, seed0 = WORKLOADS[name]
+  process, init, extra, kwds, keys, g = _build(name)
+  args = (init,) if extra is None else (init, extra)
+  thin = 1 if name == 'gibbs8' else 2
+  a = process.sampler(*args, stop=2 * t, chains=n, seeds=g['seeds'], thin=thin, **kwds)
+  b = process.sampler(*args, stop=2 * t, chains=n, seeds=g['seeds'], thin=thin, **kwds)
+  wa = list(process.walk(a, stop=stop))
+  wb = []
+  for s in b:
+    if stop is not None and len(wb) >= stop:
+      break
+    wb.append(s)
+  assert len(wa) == len(wb)
+  assert process.get_counter(a) == process.get_counter(b)
+  for sa, sb in zip(wa, wb):
+    for k in keys:
+      np.testing.assert_array_equal(np.asarray(sa.v[k]), np.asarray(sb.v[k]))
+  la, lb = process.get_last(a), process.get_last(b)
+  assert (la is None) == (lb is None)   # a walk to the end resets (sp_utils.py:14-16)
+  for k in keys if la is not None else ():
+    np.testing.assert_array_equal(np.asarray(la.p[k]), np.asarray(lb.p[k]))
+  if stop is not None:   # both continue from the step handed out last
+    na, nb = next(a), next(b)
+    for k in keys:
+      np.testing.assert_array_equal(np.asarray(na.v[k]), np.asarray(nb.v[k]))
+  a.close()
+  b.close()
+
+
+@pytest.mark.gpu
+def test_engines_reusing_cached_buffers_run_the_same_chains():
+  """A destroyed engine's buffers and stream serve the next engine
+  (pbh_cache_*): cached memory holds the old engine's data, and a run on it
+  equals a run on fresh memory bit for bit."""
+  from probayes_amd import Engine
+  import bench
+  out = []
+  for rep in range(3):
+    eng = Engine(bench.cfg2_spec())
+    eng.init_chains(np.zeros((1000, 10)))
+    eng.set_rng('philox', seed=11)
+    eng.alloc_trace(40, 1)
+    eng.run(40, steps_per_launch=16)
+    out.append(eng.trace())
+    if rep == 0:
+      eng.close()
+      Engine.cache_release()       # the second engine starts from fresh memory
+    else:
+      eng.close()                   # the third takes the second's buffers
+  idle, hits, misses = Engine.cache_info()
+  assert hits > 0 and idle > 0
+  for k in out[0]:
+    if out[0][k] is not None:
+      np.testing.assert_array_equal(np.asarray(out[0][k]), np.asarray(out[1][k]))
+      np.testing.assert_array_equal(np.asarray(out[0][k]), np.asarray(out[2][k]))
