@@ -1344,21 +1344,55 @@ class Sampler:
     self._cur, self._j = None, 0
 
   # ---- summaries -------------------------------------------------------------
-  def _gather(self, steps, get):
-    """[N, len(steps), ...] from get(block) [N, T, ...] at the steps'
-    records, one fancy index per run of steps from the same block."""
-    parts, i = [], 0
+  @staticmethod
+  def _runs(steps):
+    """(block, record indices) per run of consecutive steps from one block."""
+    i = 0
     while i < len(steps):
       b = steps[i].block
       k = i
       while k < len(steps) and steps[k].block is b:
         k += 1
-      js = np.array([s.j for s in steps[i:k]])
-      a = get(b)
-      parts.append(None if a is None else a[:, js])
+      yield b, np.array([s.j for s in steps[i:k]])
       i = k
-    if any(p is None for p in parts):
-      return None
+
+  @staticmethod
+  def _span(js):
+    """js as a slice when it is a contiguous ascending range (a walk's steps
+    are): the summary then holds views of the host trace, not copies."""
+    if len(js) and js[-1] - js[0] + 1 == len(js) and np.all(np.diff(js) == 1):
+      return slice(int(js[0]), int(js[-1]) + 1)
+    return js
+
+  def _gather(self, steps, get):
+    """[N, len(steps), ...] from get(block) [N, T, ...] at the steps'
+    records: a view for one contiguous run (a whole walk of one block), one
+    index per run of steps from the same block otherwise."""
+    parts = []
+    for b, js in self._runs(steps):
+      a = get(b)
+      if a is None:
+        return None
+      parts.append(a[:, self._span(js)])
+    if len(parts) == 1:
+      return parts[0]
+    return np.concatenate(parts, axis=1)
+
+  def _gather_prev(self, steps, key):
+    """The state before each step (its predecessor record, or the block's
+    prev for a block's record 0): key 'x' -> [N, len, d], 'p' -> [N, len];
+    a view of the records when no step is a block's record 0."""
+    parts = []
+    for b, js in self._runs(steps):
+      a = b.tr['v_' + key]
+      sp = self._span(js)
+      if isinstance(sp, slice) and sp.start >= 1:
+        parts.append(a[:, sp.start - 1:sp.stop - 1])
+        continue
+      prev = b.prev_x[:, None, :] if key == 'x' else b.prev_p[:, None]
+      parts.append(np.concatenate([prev, a[:, :-1]], 1)[:, js])
+    if len(parts) == 1:
+      return parts[0]
     return np.concatenate(parts, axis=1)
 
   def summary(self, steps):
@@ -1399,19 +1433,17 @@ class Sampler:
     if self.spec.get('kind') == 'linreg' or self.spec['scores'] == 'gibbs':
       return None, None, None
     # the state before each step: the previous record, or the block's prev
-    prev_x = lambda b: np.concatenate([b.prev_x[:, None, :], b.tr['v_x'][:, :-1]], 1)
-    prev_p = lambda b: np.concatenate([b.prev_p[:, None], b.tr['v_p'][:, :-1]], 1)
     later = [st for st in steps if not (st.j == 0 and st.block.first)]
     o = None
     if later:
-      ox = self._gather(later, prev_x)
-      op = self._gather(later, prev_p)
+      ox = self._gather_prev(later, 'x')
+      op = self._gather_prev(later, 'p')
       o = PD('p', {k: sel(ox[..., i]) for i, k in enumerate(names)},
              prob=sel(op), pscale=self.pscale)
     px = self._gather(steps, lambda b: b.tr.get('p_x'))
     if px is None:
       return o, None, None
-    prev = self._gather(steps, prev_x)
+    prev = self._gather_prev(steps, 'x')
     vp = self._gather(steps, lambda b: b.tr['v_p'])
     tran = self.spec['tran']
     if self.spec['scores'] == 'metropolis' and self.sp._tran_spec() is None:
