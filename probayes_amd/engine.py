@@ -95,6 +95,19 @@ def _close_live_engines():
       pass
 
 
+def unpack_accept(acc, n):
+  """Accept words [T, W] (uint64, bit c % 64 of word c // 64 = chain c) as
+  u [N, T] uint8, C-contiguous.  The words are transposed first ([W, T]: 8
+  bytes per 64 chains and record) and then unpacked along the chain axis --
+  transposing the unpacked [T, N] bytes instead took ~2.8 s at 65 536 chains
+  x 1 000 records (a strided read per byte)."""
+  acc = np.ascontiguousarray(acc, np.uint64)
+  count, W = acc.shape
+  by = np.ascontiguousarray(
+      np.ascontiguousarray(acc.T).view(np.uint8).reshape(W, count, 8).transpose(0, 2, 1))
+  return np.unpackbits(by, axis=1, bitorder='little').reshape(W * 64, count)[:n]
+
+
 class Engine:
   """One libpbhip engine on one device, running one lowered model."""
 
@@ -500,14 +513,7 @@ class Engine:
               _dp(x), _dp(lp), acc.ctypes.data_as(_c.POINTER(_c.c_uint64)),
               _dp(px) if debug else nul, _dp(pp) if debug else nul,
               _dp(sc) if debug else nul)
-    # u [N, T]: the accept words transposed first ([W, T], 8 B per 64 chains
-    # and record), then unpacked along the chain axis -- transposing the
-    # unpacked [T, N] bytes instead was ~2.8 s at 65 536 x 1 000 (a strided
-    # read per byte)
-    by = np.ascontiguousarray(
-        np.ascontiguousarray(acc.T).view(np.uint8).reshape(W, count, 8).transpose(0, 2, 1))
-    u = np.unpackbits(by, axis=1, bitorder='little').reshape(W * 64, count)[:n]
-    out = {'v_x': x.transpose(2, 0, 1), 'v_p': lp.T, 'u': u}
+    out = {'v_x': x.transpose(2, 0, 1), 'v_p': lp.T, 'u': unpack_accept(acc, n)}
     if debug:
       out.update({'p_x': px.transpose(2, 0, 1), 'p_p': pp.T, 's': sc.T})
     return out
