@@ -1338,9 +1338,36 @@ int pbh_legacy_replay(pbh_engine *e, int64_t n_steps) {
   // The state (position, block, pending gauss) persists between launches, so
   // the split is invisible in the stream.
   constexpr int64_t kLegacyLaunchSteps = int64_t(1) << 20;
+  // the twist-ahead pass (as pbh_legacy_run) for the chain-per-lane Mt4
+  // generator -- Gibbs rows, per-variable deltas, raw draws, odd positions;
+  // the word-parallel generator twists in its own LDS.  Words per step: Gibbs
+  // at most 2R, per-variable at least 2 per draw (randint's masked
+  // rejections beyond that twist in the generator), raw 2(d + 1), normal the
+  // polar method's mean + 8 sigma
+  const bool wp_path = a.wp && !a.gibbs && !a.vardelta;
+  const bool ahead = e->legacy_ahead && e->mt_mode == 2 && !wp_path;
+  const double dd = (double)e->d;
+  auto ahead_words = [&](int64_t m) {
+    const double mm = (double)m;
+    if (a.gibbs) return 2.0 * (mm * R + 2.0);
+    if (a.vardelta || !a.normal) return 2.0 * (mm * (dd + 1.0) + 2.0);
+    return 2.0 * (mm * (4.0 * dd / 3.14159265358979 + 1.0) +
+                  8.0 * std::sqrt(mm * 4.0 * 0.3480 * dd / 2.0) + 2.0);
+  };
+  int64_t k_fit = kLegacyLaunchSteps;
+  if (ahead) {
+    k_fit = std::min<int64_t>(n_steps, kLegacyLaunchSteps);
+    while (k_fit > 1 && ahead_words(k_fit) > 14.0 * pbh_mt_block_words()) k_fit = k_fit * 7 / 8;
+  }
   hipError_t err = hipSuccess;
   for (int64_t done = 0; done < n_steps && err == hipSuccess;) {
-    const int64_t k = std::min(n_steps - done, kLegacyLaunchSteps);
+    const int64_t k = std::min(std::min(n_steps - done, kLegacyLaunchSteps), k_fit);
+    if (ahead) {
+      const int32_t want = std::min<int32_t>(
+          15, 1 + (int32_t)std::ceil(ahead_words(k) / pbh_mt_block_words()));
+      err = pbh::launch_legacy_ahead(e->mt_key, e->mt_pos, n, want, e->stream);
+      if (err != hipSuccess) break;
+    }
     a.out = e->rep + (size_t)done * R * n;
     a.n_steps = k;
     a.step0 = e->g + done;
